@@ -1,0 +1,152 @@
+/*
+ * surfcascade.h -- C ABI of the MI355X-native SURF-cascade detect path.
+ *
+ * The reference (mrgloom/SurfCascade) has no FFI; its de-facto API is the
+ * in-process C++ classes used by ObjDetector's --detect branch.  Each entry
+ * point below names the reference interface it replaces:
+ *
+ *   Model(string cfg) + Model::Load(CascadeClassifier&)   Model.h:15-18,
+ *                                                          Model.cpp:97-194
+ *   Model::Save(CascadeClassifier&)                        Model.cpp:21-95
+ *   StageClassifier::theta, LogisticRegression::{w,        StageClassifier.h:24,
+ *     patch_index, model_->bias}                           LogisticRegression.h:16-21
+ *   CascadeClassifier::GetFittedPatchIndexes               CascadeClassifier.cpp:83-91
+ *   DenseSURFFeatureExtractor::ExtractPatches              DenseSURFFeatureExtractor.cpp:49-63
+ *   DenseSURFFeatureExtractor::IntegralImage + the scan    DenseSURFFeatureExtractor.cpp:65-87,
+ *     loop (sum / ProjectPatches / CalcFeature /           ObjDetector.cpp:160-220
+ *     CascadeClassifier::Predict2) for one image
+ *
+ * Conventions: every function returns an int status (SC_OK = 0, negative =
+ * error class) and sets a thread-local message readable via sc_last_error();
+ * no C++ exception crosses the ABI.  The caller owns input and output
+ * buffers; the library owns device memory.  One HIP stream per detector;
+ * distinct detectors may be used from different threads, one detector is not
+ * thread-safe.  Raw windows come back sorted by (frame, level, y, x) -- the
+ * reference's own order is nondeterministic (omp critical, ObjDetector.cpp:205).
+ * Model loading is strict: a missing key or a type mismatch is an error
+ * (the reference silently keeps a partial cascade, Model.cpp:188-191).
+ */
+#ifndef SURFCASCADE_H
+#define SURFCASCADE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SC_OK 0
+#define SC_ERR_INVALID (-1)  /* bad argument / unsupported geometry         */
+#define SC_ERR_IO (-2)       /* file I/O        (Model.cpp:106-110)         */
+#define SC_ERR_PARSE (-3)    /* syntax          (Model.cpp:111-116)         */
+#define SC_ERR_MODEL (-4)    /* missing key or type mismatch                */
+#define SC_ERR_DEVICE (-5)   /* HIP runtime error / no usable gfx950 device */
+#define SC_ERR_CAPACITY (-6) /* output too small; *n_out = required count   */
+#define SC_ERR_NOMEM (-7)
+
+typedef struct sc_model sc_model;
+typedef struct sc_detector sc_detector;
+
+/* Scan parameters; defaults are the reference's compile-time constants. */
+typedef struct {
+    int base_len;        /* 70    window side at level 0 (ObjDetector.cpp:104) */
+    double scale_factor; /* 1.1   l_i = (int)(base_len*pow(1.1,i)) (:180)      */
+    int n_levels;        /* -1 => (int)min(log(W/70f)/log1.1, ...)+1 (:174)    */
+    int step;            /* 0  => base_len>20 ? base_len/20 : 1 (:139)         */
+    float prefilter_k;   /* 6     sum(win) > area*6 (:188)                     */
+    double stride_score; /* 0.5   multi = score<0.5 ? 2 : 1 (:214)             */
+    int tmpl_w, tmpl_h;  /* 40x40 template (:112)                              */
+    int aspect_h;        /* 1; window height = aspect_h*l (2 for 64x128 ext.)  */
+} sc_scan_params;
+
+/* One raw (pre-groupRectangles) detection, ObjDetector.cpp:203-208. */
+typedef struct {
+    int32_t level, x, y, w, h;
+    int32_t stage_reached; /* == number of stages for a detection          */
+    double score;          /* ((double)s_last + p + 1) / S  (:201)          */
+} sc_window;
+
+/* Device-side record written by sc_enqueue_device (40 bytes). */
+typedef struct {
+    int32_t frame, level, x, y, w, h, stage_reached, _pad;
+    double score;
+} sc_det_record;
+
+void sc_scan_params_default(sc_scan_params *p);
+
+/* ---- model (Model.cpp) ------------------------------------------------- */
+int sc_model_load(const char *cfg_path, sc_model **out);
+int sc_model_parse(const char *text, size_t len, sc_model **out);
+int sc_model_save(const sc_model *m, const char *cfg_path);
+int sc_model_num_stages(const sc_model *m);
+int sc_model_stage(const sc_model *m, int stage, float *theta, int *n_weak);
+int sc_model_weak(const sc_model *m, int stage, int k, int *patch_index,
+                  float w33[33], double *bias);
+void sc_model_free(sc_model *m);
+
+/* ---- template patches (DenseSURFFeatureExtractor::ExtractPatches) ------- */
+int sc_extract_patches(int tmpl_w, int tmpl_h, int32_t *rects_xywh, int cap);
+
+/* ---- detector ----------------------------------------------------------- */
+int sc_detector_create(const char *cfg_path, const sc_scan_params *p,
+                       int device, sc_detector **out);
+int sc_detector_create_from_model(const sc_model *m, const sc_scan_params *p,
+                                  int device, sc_detector **out);
+void sc_detector_destroy(sc_detector *d);
+
+/* One host frame -> raw windows (sorted).  *n_out = total count even when it
+ * exceeds capacity (then SC_ERR_CAPACITY and the first `capacity` stored). */
+int sc_detect(sc_detector *d, const uint8_t *gray, int w, int h,
+              int stride_bytes, sc_window *out, int capacity, int *n_out);
+/* n host frames of one size.  out holds all frames' windows back to back;
+ * n_out[f] = count for frame f. */
+int sc_detect_batch(sc_detector *d, const uint8_t *const *frames, int n,
+                    int w, int h, int stride_bytes, sc_window *out,
+                    int capacity, int *n_out);
+/* n frames already in device memory (frame f at d_frames + f*h*stride). */
+int sc_detect_device(sc_detector *d, const uint8_t *d_frames, int n, int w,
+                     int h, int stride_bytes, sc_window *out, int capacity,
+                     int *n_out);
+/* Asynchronous form on the detector's stream: device records (unsorted;
+ * canonical order = sort by frame, level, y, x) + device counters
+ * d_counts[0] = total, d_counts[1+f] = frame f's count.  No host sync. */
+int sc_enqueue_device(sc_detector *d, const uint8_t *d_frames, int n, int w,
+                      int h, int stride_bytes, sc_det_record *d_out,
+                      int capacity, int32_t *d_counts);
+int sc_synchronize(sc_detector *d);
+void *sc_detector_stream(sc_detector *d); /* hipStream_t */
+
+/* ---- introspection / parity dumps -------------------------------------- */
+#define SC_INFO_LEVELS 1        /* levels used for the last geometry         */
+#define SC_INFO_GRID_WINDOWS 2  /* stride-step grid windows per frame        */
+#define SC_INFO_ROWS 3          /* (level, y) rows per frame                 */
+#define SC_INFO_TABLE_PITCH 4   /* integral-table row pitch in cells         */
+#define SC_INFO_VISITED 5       /* windows the adaptive stride visited (last) */
+int sc_detector_info(sc_detector *d, int what, int64_t *value);
+
+/* Enable per-window debug records (grid order) for the next detect calls. */
+int sc_detector_set_debug(sc_detector *d, int on);
+#define SC_DUMP_INTEGRAL 1    /* float[(H+1)*(W+1)*8] of frame `frame`       */
+#define SC_DUMP_GRID_STAGE 2  /* int16[grid]: p (-1 = prefilter reject)      */
+#define SC_DUMP_GRID_SCORE 3  /* float[grid]: last stage score               */
+#define SC_DUMP_GRID_VISIT 4  /* uint8[grid]: 1 = visited by the x chain     */
+int sc_debug_dump(sc_detector *d, int what, int frame, void *dst,
+                  size_t bytes);
+
+/* Per-kernel HIP-event timing on the detector's stream (bench / profiling). */
+#define SC_KERNEL_ROWSCAN 0
+#define SC_KERNEL_COLSCAN 1
+#define SC_KERNEL_WINDOWS 2
+#define SC_KERNEL_COUNT 3
+int sc_set_timing(sc_detector *d, int on);
+int sc_get_timing(sc_detector *d, double ms_total[SC_KERNEL_COUNT],
+                  int64_t launches[SC_KERNEL_COUNT]);
+
+const char *sc_last_error(void);
+const char *sc_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SURFCASCADE_H */

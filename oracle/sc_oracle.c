@@ -1,0 +1,407 @@
+/*
+ * sc_oracle.c -- CPU restatement of the SurfCascade detect path
+ * (TEST INFRASTRUCTURE ONLY -- see sc_oracle.h for the rules and the parity
+ * status).  Scalar C; every f32/f64 operation is written in the association
+ * order the reference's SSE code imposes.  Build with -ffp-contract=off and
+ * without -ffast-math (oracle/Makefile) so each C operator is one IEEE op.
+ */
+#include "sc_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ----------------------------------------------------------------------- */
+/* Scan geometry                                                            */
+/* ----------------------------------------------------------------------- */
+
+/* l = (int)(70 * pow(1.1, i)) in f64 -- ObjDetector.cpp:180. */
+int sco_level_len(int base, int i) { return (int)(base * pow(1.1, i)); }
+
+/* (int)min(log(W/(float)70)/log(1.1), log(H/(float)70)/log(1.1)) + 1 levels
+ * (the loop at ObjDetector.cpp:178 is inclusive).  log() of a float argument
+ * resolves to the float overload in MSVC C++ (ObjDetector.cpp:174). */
+int sco_num_levels(int W, int H, int base_w, int base_h) {
+    double a = logf((float)W / (float)base_w) / log(1.1);
+    double b = logf((float)H / (float)base_h) / log(1.1);
+    return (int)(a < b ? a : b) + 1;
+}
+
+/* step = win.width > 20 ? win.width / 20 : 1 -- ObjDetector.cpp:139. */
+int sco_step(const sco_params *p) {
+    if (p->step > 0) return p->step;
+    return p->base_len > 20 ? p->base_len / 20 : 1;
+}
+
+int sco_effective_levels(int W, int H, const sco_params *p) {
+    if (p->n_levels >= 0) return p->n_levels;
+    return sco_num_levels(W, H, p->base_len, p->base_len * p->aspect_h);
+}
+
+int64_t sco_grid_count(int W, int H, const sco_params *p) {
+    int st = sco_step(p), nl = sco_effective_levels(W, H, p);
+    int64_t n = 0;
+    for (int i = 0; i < nl; i++) {
+        int l = sco_level_len(p->base_len, i), lh = l * p->aspect_h;
+        if (l > W || lh > H) continue;
+        n += (int64_t)((W - l) / st + 1) * ((H - lh) / st + 1);
+    }
+    return n;
+}
+
+/* Dense template patches -- DenseSURFFeatureExtractor.cpp:21,49-63 and
+ * constants .h:31-35: shapes {2x2, 1x4, 4x1}, cell edge 6..W/2, stride 4. */
+int sco_extract_patches(int tw, int th, int32_t *rects, int cap) {
+    static const int shp[3][2] = {{2, 2}, {1, 4}, {4, 1}};
+    int n = 0;
+    for (int j = 0; j < 3; j++)
+        for (int c = 6; c <= tw / 2; c++) {
+            int pw = shp[j][0] * c, ph = shp[j][1] * c;
+            for (int y = 0; y + ph <= th; y += 4)
+                for (int x = 0; x + pw <= tw; x += 4) {
+                    if (rects && n < cap) {
+                        rects[4 * n + 0] = x;
+                        rects[4 * n + 1] = y;
+                        rects[4 * n + 2] = pw;
+                        rects[4 * n + 3] = ph;
+                    }
+                    n++;
+                }
+        }
+    return n;
+}
+
+/* ----------------------------------------------------------------------- */
+/* Gradient planes + integral table                                         */
+/* ----------------------------------------------------------------------- */
+
+static inline uint8_t sat_sub(int a, int b) { return (uint8_t)(a > b ? a - b : 0); }
+
+/* T2bFilter -- DenseSURFFeatureExtractor.cpp:199-349.  For each direction k
+ * the pair (Ip, In) gives plane 2k = sat(Ip - In) = (|d|-d)/2 and plane
+ * 2k+1 = sat(In - Ip) = (|d|+d)/2 with d = In - Ip.  Edge handling of the
+ * reference reduces to clamping the neighbour coordinates:
+ *   dx (:224-254)  In = I[y][x+1]      Ip = I[y][x-1]
+ *   dy (:256-281)  In = I[y+1][x]      Ip = I[y-1][x]
+ *   du (:283-314)  In = I[y+1][x+1]    Ip = I[y-1][x-1]
+ *   dv (:316-347)  In = I[y-1][x+1]    Ip = I[y+1][x-1]
+ * (W, H >= 2). */
+void sco_gradients(const uint8_t *img, int W, int H, int stride, uint8_t *g) {
+    const size_t sz = (size_t)W * H;
+    for (int y = 0; y < H; y++) {
+        const uint8_t *c = img + (size_t)y * stride;
+        const uint8_t *u = img + (size_t)(y > 0 ? y - 1 : 0) * stride;
+        const uint8_t *d = img + (size_t)(y < H - 1 ? y + 1 : H - 1) * stride;
+        for (int x = 0; x < W; x++) {
+            int xn = x < W - 1 ? x + 1 : W - 1, xp = x > 0 ? x - 1 : 0;
+            size_t o = (size_t)y * W + x;
+            int in, ip;
+            in = c[xn]; ip = c[xp];
+            g[0 * sz + o] = sat_sub(ip, in); g[1 * sz + o] = sat_sub(in, ip);
+            in = d[x]; ip = u[x];
+            g[2 * sz + o] = sat_sub(ip, in); g[3 * sz + o] = sat_sub(in, ip);
+            in = d[xn]; ip = u[xp];
+            g[4 * sz + o] = sat_sub(ip, in); g[5 * sz + o] = sat_sub(in, ip);
+            in = u[xn]; ip = d[xp];
+            g[6 * sz + o] = sat_sub(ip, in); g[7 * sz + o] = sat_sub(in, ip);
+        }
+    }
+}
+
+/* IntegralImage -- DenseSURFFeatureExtractor.cpp:65-87: cv::integral
+ * (8U -> 32F) per plane, then cv::merge into the 8-float-per-cell table
+ * (F256Dat, .h:21-25).  OpenCV's scalar integral_ keeps the running row sum
+ * s in the sum type (f32, exact here since s <= 255*W < 2^24) and forms
+ * S[y+1][x+1] = S[y][x+1] + s as one f32 add, sequential in y.
+ * T has (H+1) rows of (W+1) cells of 8 floats. */
+void sco_integral(const uint8_t *img, int W, int H, int stride, float *T) {
+    const size_t sz = (size_t)W * H, pitch = (size_t)(W + 1) * 8;
+    uint8_t *g = (uint8_t *)malloc(8 * sz);
+    sco_gradients(img, W, H, stride, g);
+    memset(T, 0, pitch * sizeof(float));
+    for (int y = 0; y < H; y++) {
+        float *prev = T + (size_t)y * pitch, *row = T + (size_t)(y + 1) * pitch;
+        for (int ch = 0; ch < 8; ch++) {
+            const uint8_t *gr = g + ch * sz + (size_t)y * W;
+            float s = 0.0f;
+            row[ch] = 0.0f;
+            for (int x = 0; x < W; x++) {
+                s += (float)gr[x];
+                row[(size_t)(x + 1) * 8 + ch] = prev[(size_t)(x + 1) * 8 + ch] + s;
+            }
+        }
+    }
+    free(g);
+}
+
+/* ----------------------------------------------------------------------- */
+/* Window arithmetic                                                        */
+/* ----------------------------------------------------------------------- */
+
+#define CELL(T, W, yy, xx) ((T) + ((size_t)(yy) * (size_t)((W) + 1) + (size_t)(xx)) * 8)
+
+/* sum(win) -- DenseSURFFeatureExtractor.cpp:351-358 (xmm_f1 = channels 0-3,
+ * (A+D)-(B+C) per lane, then ((s0+s1)+s2)+s3, /2), compared at
+ * ObjDetector.cpp:188 against win.area()*6 converted to float. */
+int sco_prefilter(const float *T, int W, int x, int y, int w, int h, float k,
+                  float *m_out) {
+    const float *tl = CELL(T, W, y, x), *br = CELL(T, W, y + h, x + w);
+    const float *tr = CELL(T, W, y, x + w), *bl = CELL(T, W, y + h, x);
+    float v[4];
+    for (int c = 0; c < 4; c++) v[c] = (tl[c] + br[c]) - (tr[c] + bl[c]);
+    float m = (((v[0] + v[1]) + v[2]) + v[3]) / 2.0f;
+    if (m_out) *m_out = m;
+    float thr = (float)(w * h) * k;
+    return m > thr;
+}
+
+/* ProjectPatches -- DenseSURFFeatureExtractor.cpp:459-484.  scale is
+ * (float)l / tmpl_w (f32 division); coordinates truncate toward zero. */
+void sco_project(const int32_t tr[4], float scale, int wx, int wy,
+                 int32_t out[4]) {
+    out[0] = (int)((float)tr[0] * scale) + wx;
+    out[1] = (int)((float)tr[1] * scale) + wy;
+    if (tr[2] >= tr[3]) {
+        int ratio = tr[2] / tr[3];
+        out[3] = (int)((float)tr[3] * scale);
+        out[2] = out[3] * ratio;
+    } else {
+        int ratio = tr[3] / tr[2];
+        out[2] = (int)((float)tr[2] * scale);
+        out[3] = out[2] * ratio;
+    }
+}
+
+/* SSE3 hadd-ordered sum of squares with lane-3 seed FLT_EPSILON --
+ * DenseSURFFeatureExtractor.cpp:427-433: c_k = (q0+q1)+(q2+q3) per quad,
+ * SS = (((eps + c0) + c1) + ...) + c7. */
+static float ss_hadd(const float f[32]) {
+    float ss = FLT_EPSILON;
+    for (int k = 0; k < 8; k++) {
+        float q0 = f[4 * k] * f[4 * k], q1 = f[4 * k + 1] * f[4 * k + 1];
+        float q2 = f[4 * k + 2] * f[4 * k + 2], q3 = f[4 * k + 3] * f[4 * k + 3];
+        float ck = (q0 + q1) + (q2 + q3);
+        ss = ss + ck;
+    }
+    return ss;
+}
+
+/* Normalize -- DenseSURFFeatureExtractor.cpp:417-457; theta = 2/sqrt(32)
+ * (.h:36).  _mm_min_ps(a,b) = a<b?a:b and _mm_max_ps(a,b) = a>b?a:b. */
+void sco_normalize(float f[32]) {
+    const float theta = 2.0f / sqrtf(32.0f);
+    float t = sqrtf(ss_hadd(f)) * theta, nt = -t;
+    for (int i = 0; i < 32; i++) {
+        float v = f[i] < t ? f[i] : t;
+        f[i] = v > nt ? v : nt;
+    }
+    float r = 1.0f / sqrtf(ss_hadd(f));
+    for (int i = 0; i < 32; i++) f[i] = f[i] * r;
+}
+
+/* GetRectsFromPatch (:360-377) + CalcFeature (:379-415): four cells,
+ * feature[8*cell + ch] = (TL + BR) - (TR + BL), then Normalize. */
+void sco_calc_feature(const float *T, int W, const int32_t r[4], float f[32]) {
+    int ce = (r[2] == r[3]) ? r[2] / 2 : (r[2] < r[3] ? r[2] : r[3]);
+    int gw = r[2] / ce, gh = r[3] / ce;
+    for (int hh = 0; hh < gh; hh++)
+        for (int ww = 0; ww < gw; ww++) {
+            int cell = hh * gw + ww;
+            int x0 = r[0] + ww * ce, y0 = r[1] + hh * ce;
+            const float *tl = CELL(T, W, y0, x0), *br = CELL(T, W, y0 + ce, x0 + ce);
+            const float *tr = CELL(T, W, y0, x0 + ce), *bl = CELL(T, W, y0 + ce, x0);
+            for (int c = 0; c < 8; c++)
+                f[8 * cell + c] = (tl[c] + br[c]) - (tr[c] + bl[c]);
+        }
+    sco_normalize(f);
+}
+
+/* LogisticRegression::Predict -- LogisticRegression.cpp:46-68: four f32
+ * lane accumulators over i = 0,4,..,28, two hadds, then f64:
+ * z += w[32]*bias, p = 1/(1+exp(-z)), returned as float. */
+float sco_lr_predict(const float *w, double bias, const float f[32]) {
+    float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int i = 0; i < 32; i += 4)
+        for (int j = 0; j < 4; j++) s[j] = w[i + j] * f[i + j] + s[j];
+    float z32 = (s[0] + s[1]) + (s[2] + s[3]);
+    double prob = (double)z32;
+    prob += (double)w[32] * bias;
+    prob = 1.0 / (1.0 + exp(-prob));
+    return (float)prob;
+}
+
+/* GentleAdaboost::Predict2 -- GentleAdaboost.cpp:247-261: f32 sum in weak
+ * order, divided by (float)n. */
+static float stage_score(const float *T, int W, const sco_model *m, int s,
+                         int64_t off, float scale, int x, int y) {
+    float sum = 0.0f;
+    for (int k = 0; k < m->n_weak[s]; k++) {
+        int32_t pr[4];
+        float f[32];
+        sco_project(m->patch + 4 * (off + k), scale, x, y, pr);
+        sco_calc_feature(T, W, pr, f);
+        sum += sco_lr_predict(m->w + 33 * (off + k), m->bias[off + k], f);
+    }
+    return sum / (float)m->n_weak[s];
+}
+
+/* One window of the detect loop, ObjDetector.cpp:188-201: prefilter, then
+ * stages until the first stage whose score < theta.  Returns p (the failing
+ * stage, n_stages if all pass, -1 if the prefilter rejects); *s_last gets the
+ * last evaluated stage score. */
+int sco_eval_window(const float *T, int W, const sco_model *m, int l, int lh,
+                    int x, int y, float k, float *s_last, float *stage_scores) {
+    if (!sco_prefilter(T, W, x, y, l, lh, k, NULL)) return -1;
+    float scale = (float)l / (float)m->tmpl_w;
+    int p;
+    float score = 0.0f;
+    int64_t off = 0;
+    for (p = 0; p < m->n_stages; p++) {
+        score = stage_score(T, W, m, p, off, scale, x, y);
+        if (stage_scores) stage_scores[p] = score;
+        off += m->n_weak[p];
+        if ((double)score < (double)m->theta[p]) break;
+    }
+    if (s_last) *s_last = score;
+    return p;
+}
+
+/* Every stage score of a window, no early exit (threshold calibration). */
+void sco_all_stage_scores(const float *T, int W, const sco_model *m, int l,
+                          int x, int y, float *out) {
+    float scale = (float)l / (float)m->tmpl_w;
+    int64_t off = 0;
+    for (int s = 0; s < m->n_stages; s++) {
+        out[s] = stage_score(T, W, m, s, off, scale, x, y);
+        off += m->n_weak[s];
+    }
+}
+
+/* Score of one stage for a batch of windows (l[i], x[i], y[i]); used to
+ * calibrate the synthetic models' thetas (tests/golden/make_models.py). */
+void sco_stage_score_batch(const float *T, int W, const sco_model *m,
+                           const int32_t *l, const int32_t *x, const int32_t *y,
+                           int64_t n, int stage, float *out, int nthreads) {
+    int64_t off = 0;
+    for (int s = 0; s < stage; s++) off += m->n_weak[s];
+    (void)nthreads;
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int64_t i = 0; i < n; i++) {
+        float scale = (float)l[i] / (float)m->tmpl_w;
+        out[i] = stage_score(T, W, m, stage, off, scale, x[i], y[i]);
+    }
+}
+
+/* final = (score + p + 1) / S in f64 -- ObjDetector.cpp:201. */
+static double final_score(float s_last, int p, int S) {
+    return ((double)s_last + p + 1) / S;
+}
+
+/* Every window of the stride-step grid (all levels), canonical order
+ * (level, y, x): p_out = stage reached (-1 = prefilter reject), s_out = last
+ * stage score (0 for prefilter rejects). */
+int64_t sco_eval_grid(const float *T, int W, int H, const sco_model *m,
+                      const sco_params *p, int16_t *p_out, float *s_out,
+                      int nthreads) {
+    int st = sco_step(p), nl = sco_effective_levels(W, H, p);
+    int64_t *base = (int64_t *)calloc((size_t)nl + 1, sizeof(int64_t));
+    for (int i = 0; i < nl; i++) {
+        int l = sco_level_len(p->base_len, i), lh = l * p->aspect_h;
+        int64_t n = (l > W || lh > H) ? 0 : (int64_t)((W - l) / st + 1) * ((H - lh) / st + 1);
+        base[i + 1] = base[i] + n;
+    }
+    int64_t total = base[nl];
+    (void)nthreads;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int i = 0; i < nl; i++) {
+        int l = sco_level_len(p->base_len, i), lh = l * p->aspect_h;
+        if (l > W || lh > H) continue;
+        int nx = (W - l) / st + 1;
+        int64_t o = base[i];
+        for (int y = 0; y <= H - lh; y += st)
+            for (int xi = 0; xi < nx; xi++, o++) {
+                float s = 0.0f;
+                int pr = sco_eval_window(T, W, m, l, lh, xi * st, y, p->prefilter_k, &s, NULL);
+                p_out[o] = (int16_t)pr;
+                s_out[o] = pr < 0 ? 0.0f : s;
+            }
+    }
+    free(base);
+    return total;
+}
+
+static int cmp_window(const void *a, const void *b) {
+    const sco_window *u = (const sco_window *)a, *v = (const sco_window *)b;
+    if (u->level != v->level) return u->level < v->level ? -1 : 1;
+    if (u->y != v->y) return u->y < v->y ? -1 : 1;
+    if (u->x != v->x) return u->x < v->x ? -1 : 1;
+    return 0;
+}
+
+/* The reference detect loop, ObjDetector.cpp:174-220: OpenMP over levels
+ * (static schedule, :177), rows at stride `step`, the serial x chain with
+ * the adaptive stride multi (:185-186, :214-217), detections collected under
+ * a critical section (:203-212).  Output is sorted canonically by
+ * (level, y, x) because the reference's append order is nondeterministic.
+ * Returns the number of detections (may exceed cap; only cap are stored). */
+int64_t sco_detect(const float *T, int W, int H, const sco_model *m,
+                   const sco_params *p, sco_window *out, int64_t cap,
+                   int64_t *n_visited, int nthreads) {
+    int st = sco_step(p), nl = sco_effective_levels(W, H, p);
+    const int S = m->n_stages;
+    int64_t n_det = 0, visited = 0;
+    int64_t buf_cap = 1024;
+    sco_window *buf = (sco_window *)malloc(sizeof(sco_window) * buf_cap);
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1) reduction(+ : visited)
+    for (int i = 0; i < nl; i++) {
+        int l = sco_level_len(p->base_len, i), lh = l * p->aspect_h;
+        for (int y = 0; y <= H - lh; y += st) {
+            int multi = 1;
+            for (int x = 0; x <= W - l; x += multi * st) {
+                visited++;
+                float s = 0.0f;
+                int pr = sco_eval_window(T, W, m, l, lh, x, y, p->prefilter_k, &s, NULL);
+                if (pr < 0) {
+                    multi = 2;
+                    continue;
+                }
+                double score = final_score(s, pr, S);
+                if (pr == S) {
+#pragma omp critical(sco_collect)
+                    {
+                        if (n_det == buf_cap) {
+                            buf_cap *= 2;
+                            buf = (sco_window *)realloc(buf, sizeof(sco_window) * buf_cap);
+                        }
+                        sco_window wv = {i, x, y, l, lh, pr, score};
+                        buf[n_det++] = wv;
+                    }
+                }
+                multi = (score < p->stride_score) ? 2 : 1;
+            }
+        }
+    }
+    qsort(buf, (size_t)n_det, sizeof(sco_window), cmp_window);
+    if (out) memcpy(out, buf, sizeof(sco_window) * (size_t)(n_det < cap ? n_det : cap));
+    free(buf);
+    if (n_visited) *n_visited = visited;
+    return n_det;
+}
+
+/* In-memory u8 frame -> raw detections (the reference's per-image body,
+ * ObjDetector.cpp:165-220, without decode / file I/O). */
+int64_t sco_detect_frame(const uint8_t *img, int W, int H, int stride,
+                         const sco_model *m, const sco_params *p,
+                         sco_window *out, int64_t cap, int64_t *n_visited,
+                         int nthreads, float *scratch_T) {
+    float *T = scratch_T;
+    if (!T) T = (float *)malloc(sizeof(float) * (size_t)(W + 1) * (H + 1) * 8);
+    sco_integral(img, W, H, stride, T);
+    int64_t n = sco_detect(T, W, H, m, p, out, cap, n_visited, nthreads);
+    if (!scratch_T) free(T);
+    return n;
+}

@@ -1,0 +1,360 @@
+"""surfcascade_amd -- MI355X-native SURF-cascade detect path.
+
+Python mirror of the reference's in-process API (ObjDetector/Model.h,
+CascadeClassifier/*.h) over the C ABI in include/surfcascade.h; the work
+happens in libsurfcascade.so (hand-written gfx950 HIP kernels).  There is no
+CPU fallback: if the library is missing, importing the binding raises.
+
+    casc = CascadeClassifier()
+    Model("model.cfg").Load(casc)                # Model.cpp:97-194
+    det = Detector(casc, ScanParams(n_levels=24))
+    wins = det.detect(gray_u8)                   # ObjDetector.cpp:165-220
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+__all__ = ["ScanParams", "Model", "CascadeClassifier", "StageClassifier", "LogisticRegression",
+           "Detector", "SurfCascadeError", "WINDOW_DTYPE", "RECORD_DTYPE", "library_path",
+           "load_library", "extract_patches"]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+SC_OK = 0
+ERRORS = {-1: "SC_ERR_INVALID", -2: "SC_ERR_IO", -3: "SC_ERR_PARSE", -4: "SC_ERR_MODEL",
+          -5: "SC_ERR_DEVICE", -6: "SC_ERR_CAPACITY", -7: "SC_ERR_NOMEM"}
+EXIT_SUCCESS, EXIT_FAILURE = 0, 1
+
+WINDOW_DTYPE = np.dtype([("level", "<i4"), ("x", "<i4"), ("y", "<i4"), ("w", "<i4"),
+                         ("h", "<i4"), ("stage", "<i4"), ("score", "<f8")])
+RECORD_DTYPE = np.dtype([("frame", "<i4"), ("level", "<i4"), ("x", "<i4"), ("y", "<i4"),
+                         ("w", "<i4"), ("h", "<i4"), ("stage", "<i4"), ("pad", "<i4"),
+                         ("score", "<f8")])
+
+KERNELS = ("rowscan", "colscan", "windows")
+
+# every symbol include/surfcascade.h declares
+EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_model_save",
+           "sc_model_num_stages", "sc_model_stage", "sc_model_weak", "sc_model_free",
+           "sc_extract_patches", "sc_detector_create", "sc_detector_create_from_model",
+           "sc_detector_destroy", "sc_detect", "sc_detect_batch", "sc_detect_device",
+           "sc_enqueue_device", "sc_synchronize", "sc_detector_stream", "sc_detector_info",
+           "sc_detector_set_debug", "sc_debug_dump", "sc_set_timing", "sc_get_timing",
+           "sc_last_error", "sc_version")
+
+
+class SurfCascadeError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (%d): %s" % (ERRORS.get(code, "SC_ERR"), code, msg))
+        self.code = code
+
+
+class ScanParams(ctypes.Structure):
+    """sc_scan_params; defaults = the reference's constants (ObjDetector.cpp)."""
+    _fields_ = [("base_len", ctypes.c_int), ("scale_factor", ctypes.c_double),
+                ("n_levels", ctypes.c_int), ("step", ctypes.c_int),
+                ("prefilter_k", ctypes.c_float), ("stride_score", ctypes.c_double),
+                ("tmpl_w", ctypes.c_int), ("tmpl_h", ctypes.c_int), ("aspect_h", ctypes.c_int)]
+
+    def __init__(self, **kw):
+        super().__init__()
+        d = dict(base_len=70, scale_factor=1.1, n_levels=-1, step=0, prefilter_k=6.0,
+                 stride_score=0.5, tmpl_w=40, tmpl_h=40, aspect_h=1)
+        d.update(kw)
+        for k, v in d.items():
+            setattr(self, k, v)
+
+    @classmethod
+    def pedestrian(cls, **kw):
+        """64x128 extension (hard part 7): window (l, 2l)."""
+        d = dict(base_len=64, tmpl_w=64, tmpl_h=128, aspect_h=2)
+        d.update(kw)
+        return cls(**d)
+
+
+def library_path():
+    return os.environ.get("SURFCASCADE_LIB", os.path.join(HERE, "lib", "libsurfcascade.so"))
+
+
+_lib = None
+
+
+def load_library():
+    """Load libsurfcascade.so; raises (never falls back) when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = library_path()
+    # One HIP runtime per process: torch bundles its own libamdhip64 (soname
+    # libamdhip64.so.7, NEEDED as "libamdhip64.so").  Loading torch first lets
+    # our NEEDED libamdhip64.so.7 bind to that copy instead of pulling in a
+    # second runtime from /opt/rocm (two runtimes hide the GPU from torch).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(path):
+        raise ImportError("libsurfcascade.so not built (%s); run __graft_entry__.build()" % path)
+    L = ctypes.CDLL(path)
+    vp, i32, i64, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t
+    P = ctypes.POINTER
+    L.sc_last_error.restype = ctypes.c_char_p
+    L.sc_version.restype = ctypes.c_char_p
+    L.sc_scan_params_default.argtypes = [P(ScanParams)]
+    L.sc_model_load.argtypes = [ctypes.c_char_p, P(vp)]
+    L.sc_model_parse.argtypes = [ctypes.c_char_p, sz, P(vp)]
+    L.sc_model_save.argtypes = [vp, ctypes.c_char_p]
+    L.sc_model_num_stages.argtypes = [vp]
+    L.sc_model_stage.argtypes = [vp, i32, P(ctypes.c_float), P(i32)]
+    L.sc_model_weak.argtypes = [vp, i32, i32, P(i32), P(ctypes.c_float), P(ctypes.c_double)]
+    L.sc_model_free.argtypes = [vp]
+    L.sc_model_free.restype = None
+    L.sc_extract_patches.argtypes = [i32, i32, P(ctypes.c_int32), i32]
+    L.sc_detector_create.argtypes = [ctypes.c_char_p, P(ScanParams), i32, P(vp)]
+    L.sc_detector_create_from_model.argtypes = [vp, P(ScanParams), i32, P(vp)]
+    L.sc_detector_destroy.argtypes = [vp]
+    L.sc_detector_destroy.restype = None
+    L.sc_detect.argtypes = [vp, vp, i32, i32, i32, vp, i32, P(i32)]
+    L.sc_detect_batch.argtypes = [vp, P(vp), i32, i32, i32, i32, vp, i32, P(i32)]
+    L.sc_detect_device.argtypes = [vp, vp, i32, i32, i32, i32, vp, i32, P(i32)]
+    L.sc_enqueue_device.argtypes = [vp, vp, i32, i32, i32, i32, vp, i32, vp]
+    L.sc_synchronize.argtypes = [vp]
+    L.sc_detector_stream.argtypes = [vp]
+    L.sc_detector_stream.restype = vp
+    L.sc_detector_info.argtypes = [vp, i32, P(i64)]
+    L.sc_detector_set_debug.argtypes = [vp, i32]
+    L.sc_debug_dump.argtypes = [vp, i32, i32, vp, sz]
+    L.sc_set_timing.argtypes = [vp, i32]
+    L.sc_get_timing.argtypes = [vp, P(ctypes.c_double), P(i64)]
+    _lib = L
+    return L
+
+
+def _check(rc):
+    if rc < 0:
+        raise SurfCascadeError(rc, load_library().sc_last_error().decode(errors="replace"))
+    return rc
+
+
+def extract_patches(tmpl_w=40, tmpl_h=40):
+    """DenseSURFFeatureExtractor::ExtractPatches (x, y, w, h rows)."""
+    L = load_library()
+    n = _check(L.sc_extract_patches(tmpl_w, tmpl_h, None, 0))
+    r = np.zeros((n, 4), np.int32)
+    L.sc_extract_patches(tmpl_w, tmpl_h, r.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n)
+    return r
+
+
+# ---------------------------------------------------------------------------
+# model objects (CascadeClassifier.h, StageClassifier.h, LogisticRegression.h)
+# ---------------------------------------------------------------------------
+
+class LogisticRegression:
+    def __init__(self, patch_index, w, bias):
+        self.patch_index = int(patch_index)
+        self.w = np.asarray(w, np.float32)
+        self.bias = float(bias)
+
+
+class StageClassifier:
+    def __init__(self, theta, weak_classifiers):
+        self.theta = np.float32(theta)
+        self.weak_classifiers = weak_classifiers
+
+    def GetFittedPatchIndexes(self):
+        return [wk.patch_index for wk in self.weak_classifiers]
+
+
+class CascadeClassifier:
+    def __init__(self):
+        self.stage_classifiers: list[StageClassifier] = []
+        self._handle = None
+
+    def GetFittedPatchIndexes(self):
+        """CascadeClassifier::GetFittedPatchIndexes (CascadeClassifier.cpp:83-91)."""
+        return [s.GetFittedPatchIndexes() for s in self.stage_classifiers]
+
+    def _adopt(self, handle):
+        L = load_library()
+        if self._handle:
+            L.sc_model_free(self._handle)
+        self._handle = handle
+        self.stage_classifiers = []
+        for s in range(L.sc_model_num_stages(handle)):
+            th, nw = ctypes.c_float(), ctypes.c_int()
+            _check(L.sc_model_stage(handle, s, ctypes.byref(th), ctypes.byref(nw)))
+            weaks = []
+            for k in range(nw.value):
+                pi, b = ctypes.c_int(), ctypes.c_double()
+                w = (ctypes.c_float * 33)()
+                _check(L.sc_model_weak(handle, s, k, ctypes.byref(pi), w, ctypes.byref(b)))
+                weaks.append(LogisticRegression(pi.value, np.frombuffer(w, np.float32).copy(), b.value))
+            self.stage_classifiers.append(StageClassifier(th.value, weaks))
+
+    def __del__(self):
+        if getattr(self, "_handle", None) and _lib is not None:
+            _lib.sc_model_free(self._handle)
+            self._handle = None
+
+
+class Model:
+    """Model(string cfg) with Load/Save returning EXIT_SUCCESS/EXIT_FAILURE
+    (Model.h:15-18).  Unlike the reference, Load is strict: a missing key or
+    a type mismatch fails (the message is in `last_error`)."""
+
+    def __init__(self, model_cfg):
+        self.model_cfg = str(model_cfg)
+        self.last_error = ""
+
+    def Load(self, cascade: CascadeClassifier):
+        L = load_library()
+        h = ctypes.c_void_p()
+        rc = L.sc_model_load(self.model_cfg.encode(), ctypes.byref(h))
+        if rc != SC_OK:
+            self.last_error = L.sc_last_error().decode(errors="replace")
+            self.last_code = rc
+            return EXIT_FAILURE
+        cascade._adopt(h.value)
+        return EXIT_SUCCESS
+
+    def Save(self, cascade: CascadeClassifier):
+        L = load_library()
+        if not cascade._handle:
+            self.last_error = "cascade has no loaded model"
+            return EXIT_FAILURE
+        rc = L.sc_model_save(cascade._handle, self.model_cfg.encode())
+        if rc != SC_OK:
+            self.last_error = L.sc_last_error().decode(errors="replace")
+            return EXIT_FAILURE
+        return EXIT_SUCCESS
+
+    @staticmethod
+    def parse(text: str) -> CascadeClassifier:
+        L = load_library()
+        h = ctypes.c_void_p()
+        b = text.encode()
+        _check(L.sc_model_parse(b, len(b), ctypes.byref(h)))
+        c = CascadeClassifier()
+        c._adopt(h.value)
+        return c
+
+
+# ---------------------------------------------------------------------------
+# detector
+# ---------------------------------------------------------------------------
+
+class Detector:
+    """Owns device model + buffers + one HIP stream (sc_detector)."""
+
+    def __init__(self, cascade, params: ScanParams | None = None, device: int = 0):
+        L = load_library()
+        self.params = params or ScanParams()
+        h = ctypes.c_void_p()
+        if isinstance(cascade, CascadeClassifier):
+            _check(L.sc_detector_create_from_model(cascade._handle, ctypes.byref(self.params),
+                                                   device, ctypes.byref(h)))
+        else:
+            _check(L.sc_detector_create(str(cascade).encode(), ctypes.byref(self.params), device,
+                                        ctypes.byref(h)))
+        self._h = h.value
+        self.device = device
+
+    def close(self):
+        if self._h:
+            load_library().sc_detector_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib is not None:
+            _lib.sc_detector_destroy(self._h)
+            self._h = None
+
+    # -- host frames --------------------------------------------------------
+    def detect(self, img, capacity=1 << 16):
+        img = np.ascontiguousarray(img, np.uint8)
+        H, W = img.shape
+        out = np.zeros(capacity, WINDOW_DTYPE)
+        n = ctypes.c_int()
+        _check(load_library().sc_detect(self._h, img.ctypes.data, W, H, W, out.ctypes.data,
+                                        capacity, ctypes.byref(n)))
+        return out[:n.value]
+
+    def detect_batch(self, frames, capacity=1 << 18):
+        frames = np.ascontiguousarray(frames, np.uint8)
+        nf, H, W = frames.shape
+        ptrs = (ctypes.c_void_p * nf)(*[frames[i].ctypes.data for i in range(nf)])
+        out = np.zeros(capacity, WINDOW_DTYPE)
+        counts = (ctypes.c_int * nf)()
+        _check(load_library().sc_detect_batch(self._h, ptrs, nf, W, H, W, out.ctypes.data,
+                                              capacity, counts))
+        res, o = [], 0
+        for c in counts:
+            res.append(out[o:o + c].copy())
+            o += c
+        return res
+
+    # -- device frames (torch uint8 tensor [n, H, W] on this device) --------
+    def detect_device(self, frames, capacity=1 << 18):
+        n, H, W = frames.shape
+        out = np.zeros(capacity, WINDOW_DTYPE)
+        counts = (ctypes.c_int * n)()
+        _check(load_library().sc_detect_device(self._h, frames.data_ptr(), n, W, H, W,
+                                               out.ctypes.data, capacity, counts))
+        res, o = [], 0
+        for c in counts:
+            res.append(out[o:o + c].copy())
+            o += c
+        return res
+
+    def enqueue_device(self, frames, out_records, counts):
+        """Async: out_records = torch uint8 [cap*40] (RECORD_DTYPE), counts = int32 [1+n]."""
+        n, H, W = frames.shape
+        cap = out_records.numel() * out_records.element_size() // RECORD_DTYPE.itemsize
+        _check(load_library().sc_enqueue_device(self._h, frames.data_ptr(), n, W, H, W,
+                                                out_records.data_ptr(), cap, counts.data_ptr()))
+
+    def synchronize(self):
+        _check(load_library().sc_synchronize(self._h))
+
+    @property
+    def stream_ptr(self):
+        return load_library().sc_detector_stream(self._h)
+
+    # -- introspection ---------------------------------------------------------
+    def info(self, key):
+        keys = {"levels": 1, "grid_windows": 2, "rows": 3, "table_pitch": 4, "visited": 5}
+        v = ctypes.c_int64()
+        _check(load_library().sc_detector_info(self._h, keys[key], ctypes.byref(v)))
+        return v.value
+
+    def set_debug(self, on=True):
+        _check(load_library().sc_detector_set_debug(self._h, int(on)))
+
+    def dump_integral(self, W, H, frame=0):
+        T = np.zeros((H + 1, W + 1, 8), np.float32)
+        _check(load_library().sc_debug_dump(self._h, 1, frame, T.ctypes.data, T.nbytes))
+        return T
+
+    def dump_grid(self, frame=0):
+        n = self.info("grid_windows")
+        p = np.zeros(n, np.int16)
+        s = np.zeros(n, np.float32)
+        v = np.zeros(n, np.uint8)
+        L = load_library()
+        _check(L.sc_debug_dump(self._h, 2, frame, p.ctypes.data, p.nbytes))
+        _check(L.sc_debug_dump(self._h, 3, frame, s.ctypes.data, s.nbytes))
+        _check(L.sc_debug_dump(self._h, 4, frame, v.ctypes.data, v.nbytes))
+        return p, s, v.astype(bool)
+
+    def set_timing(self, on=True):
+        _check(load_library().sc_set_timing(self._h, int(on)))
+
+    def get_timing(self):
+        ms = (ctypes.c_double * 3)()
+        n = (ctypes.c_int64 * 3)()
+        _check(load_library().sc_get_timing(self._h, ms, n))
+        return {k: (ms[i], n[i]) for i, k in enumerate(KERNELS)}

@@ -1,0 +1,702 @@
+// sc_api.cpp -- the C ABI (include/surfcascade.h): model I/O, detector
+// lifecycle, geometry tables, launches, result gathering.
+//
+// Host-side precomputation mirrors the reference's per-image setup:
+//   levels     l_i = (int)(70*pow(1.1,i)), count (int)min(log..)+1  ObjDetector.cpp:174,180
+//   step       win.width>20 ? win.width/20 : 1                      ObjDetector.cpp:139
+//   fitted patch table per stage (GetFittedPatchIndexes)            ObjDetector.cpp:119-130
+//   ProjectPatches per level (depends on l only; the window origin is an
+//   additive offset)                                                DenseSURFFeatureExtractor.cpp:459-484
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "sc_kernels.hpp"
+#include "sc_model.hpp"
+#include "surfcascade.h"
+
+using sc::Error;
+
+struct sc_model {
+    sc::Cascade c;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            throw Error{SC_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)}; \
+    } while (0)
+
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    void ensure(size_t want) {
+        if (want <= n) return;
+        release();
+        HIPCHK(hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T)));
+        n = want;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+struct Geometry {
+    int W = 0, H = 0;
+    int n_levels = 0, step = 1, pitch_cells = 0, nx_max = 0;
+    long long grid = 0;
+    std::vector<sc::LevelInfo> levels;
+    std::vector<int2> rows;
+    std::vector<sc::ProjPatch> proj;
+};
+
+}  // namespace
+
+struct sc_detector {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    sc_scan_params prm{};
+    sc::Cascade casc;
+    int K = 0, S = 0;
+    std::vector<int32_t> patch_rects;  // fitted template rect per global weak
+    // model on device
+    DevBuf<float> d_w;
+    DevBuf<double> d_bias;
+    DevBuf<float> d_theta;
+    DevBuf<int> d_stage_off;
+    // geometry on device
+    Geometry geo;
+    DevBuf<sc::LevelInfo> d_levels;
+    DevBuf<int2> d_rows;
+    DevBuf<sc::ProjPatch> d_proj;
+    // working buffers
+    DevBuf<uint8_t> d_frames;
+    DevBuf<float> d_table;
+    int table_frames = 0;
+    DevBuf<sc_det_record> d_out;
+    DevBuf<int> d_counters;
+    DevBuf<unsigned long long> d_visited;
+    // debug
+    bool debug = false;
+    DevBuf<int16_t> d_dbg_p;
+    DevBuf<float> d_dbg_s;
+    DevBuf<uint8_t> d_dbg_v;
+    int last_frames = 0;
+    long long last_visited = 0;
+    // timing
+    bool timing = false;
+    struct Pending {
+        int kind;
+        hipEvent_t a, b;
+    };
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> event_pool;
+    double t_ms[SC_KERNEL_COUNT] = {0, 0, 0};
+    long long t_n[SC_KERNEL_COUNT] = {0, 0, 0};
+
+    ~sc_detector() {
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        for (auto &p : pending) {
+            event_pool.push_back(p.a);
+            event_pool.push_back(p.b);
+        }
+        for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
+        d_w.release(); d_bias.release(); d_theta.release(); d_stage_off.release();
+        d_levels.release(); d_rows.release(); d_proj.release();
+        d_frames.release(); d_table.release(); d_out.release(); d_counters.release();
+        d_visited.release(); d_dbg_p.release(); d_dbg_s.release(); d_dbg_v.release();
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    hipEvent_t ev() {
+        if (!event_pool.empty()) {
+            hipEvent_t e = event_pool.back();
+            event_pool.pop_back();
+            return e;
+        }
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        return e;
+    }
+};
+
+namespace {
+
+int ref_step(const sc_scan_params &p) {
+    if (p.step > 0) return p.step;
+    return p.base_len > 20 ? p.base_len / 20 : 1;  // ObjDetector.cpp:139
+}
+
+// ObjDetector.cpp:174 (float log of W/(float)70, f64 division by log(1.1)) + 1.
+int ref_levels(int W, int H, const sc_scan_params &p) {
+    if (p.n_levels >= 0) return p.n_levels;
+    double a = std::log((float)W / (float)p.base_len) / std::log(p.scale_factor);
+    double b = std::log((float)H / (float)(p.base_len * p.aspect_h)) / std::log(p.scale_factor);
+    return (int)std::min(a, b) + 1;
+}
+
+void build_geometry(sc_detector *d, int W, int H) {
+    Geometry &g = d->geo;
+    if (g.W == W && g.H == H) return;
+    if (W < 2 || H < 2) throw Error{SC_ERR_INVALID, "frame must be at least 2x2"};
+    if (W > 32767 || H > 32767) throw Error{SC_ERR_INVALID, "frame dimension above 32767"};
+    const sc_scan_params &p = d->prm;
+    Geometry ng;
+    ng.W = W;
+    ng.H = H;
+    ng.step = ref_step(p);
+    ng.n_levels = ref_levels(W, H, p);
+    if (ng.n_levels < 0 || ng.n_levels > 256) throw Error{SC_ERR_INVALID, "bad level count"};
+    ng.pitch_cells = ((W + 1) + 3) & ~3;
+    ng.proj.resize((size_t)ng.n_levels * d->K);
+    long long gb = 0;
+    for (int i = 0; i < ng.n_levels; i++) {
+        sc::LevelInfo L{};
+        L.l = (int)(p.base_len * std::pow(p.scale_factor, i));  // ObjDetector.cpp:180
+        L.lh = L.l * p.aspect_h;
+        L.grid_base = gb;
+        L.thr = (float)(L.l * L.lh) * p.prefilter_k;
+        if (L.l >= 1 && L.l <= W && L.lh <= H) {
+            L.nx = (W - L.l) / ng.step + 1;
+            L.ny = (H - L.lh) / ng.step + 1;
+            if (L.nx > 65535) throw Error{SC_ERR_INVALID, "too many windows per row"};
+            for (int r = 0; r < L.ny; r++) ng.rows.push_back(make_int2(i, r * ng.step));
+            gb += (long long)L.nx * L.ny;
+            ng.nx_max = std::max(ng.nx_max, L.nx);
+        }
+        // ProjectPatches (DenseSURFFeatureExtractor.cpp:459-484) + cell split
+        // (GetRectsFromPatch :360-377) for every fitted patch at this level.
+        const float scale = (float)L.l / (float)p.tmpl_w;
+        for (int k = 0; k < d->K; k++) {
+            const int32_t *r = &d->patch_rects[4 * k];
+            int px = (int)((float)r[0] * scale), py = (int)((float)r[1] * scale), pw, ph;
+            if (r[2] >= r[3]) {
+                int ratio = r[2] / r[3];
+                ph = (int)((float)r[3] * scale);
+                pw = ph * ratio;
+            } else {
+                int ratio = r[3] / r[2];
+                pw = (int)((float)r[2] * scale);
+                ph = pw * ratio;
+            }
+            sc::ProjPatch pp{};
+            int gw, gh;
+            if (pw == ph) {
+                pp.c = (int16_t)(pw / 2);
+                pp.shape = 0;
+                gw = gh = 2;
+            } else {
+                int c = std::min(pw, ph);
+                pp.c = (int16_t)c;
+                pp.shape = pw < ph ? 1 : 2;
+                gw = pw / std::max(c, 1);
+                gh = ph / std::max(c, 1);
+            }
+            if (pp.c <= 0)
+                throw Error{SC_ERR_INVALID, "projected cell edge is 0 at level " + std::to_string(i)};
+            pp.dx = (int16_t)px;
+            pp.dy = (int16_t)py;
+            if (L.nx > 0 && (px + gw * pp.c > L.l || py + gh * pp.c > L.lh))
+                throw Error{SC_ERR_INVALID, "projected patch leaves the window at level " +
+                                                std::to_string(i)};
+            ng.proj[(size_t)i * d->K + k] = pp;
+        }
+        ng.levels.push_back(L);
+    }
+    ng.grid = gb;  // may be 0: no window fits (the reference loop runs 0 times)
+    d->d_levels.ensure(std::max<size_t>(ng.levels.size(), 1));
+    d->d_rows.ensure(std::max<size_t>(ng.rows.size(), 1));
+    d->d_proj.ensure(std::max<size_t>(ng.proj.size(), 1));
+    if (!ng.levels.empty())
+        HIPCHK(hipMemcpyAsync(d->d_levels.p, ng.levels.data(),
+                              ng.levels.size() * sizeof(sc::LevelInfo), hipMemcpyHostToDevice,
+                              d->stream));
+    if (!ng.rows.empty())
+        HIPCHK(hipMemcpyAsync(d->d_rows.p, ng.rows.data(), ng.rows.size() * sizeof(int2),
+                              hipMemcpyHostToDevice, d->stream));
+    if (!ng.proj.empty())
+        HIPCHK(hipMemcpyAsync(d->d_proj.p, ng.proj.data(), ng.proj.size() * sizeof(sc::ProjPatch),
+                              hipMemcpyHostToDevice, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));  // host vectors are re-assigned below
+    d->geo = std::move(ng);
+}
+
+void upload_model(sc_detector *d) {
+    const sc::Cascade &c = d->casc;
+    d->S = (int)c.stages.size();
+    d->K = c.total_weak();
+    std::vector<int32_t> all = sc::extract_patches(d->prm.tmpl_w, d->prm.tmpl_h);
+    sc::validate_for_detect(c, (int)all.size() / 4);
+    std::vector<float> w((size_t)d->K * 36, 0.0f);
+    std::vector<double> bias(d->K);
+    std::vector<float> theta(d->S);
+    std::vector<int> off(d->S + 1, 0);
+    d->patch_rects.assign((size_t)d->K * 4, 0);
+    int g = 0;
+    for (int s = 0; s < d->S; s++) {
+        theta[s] = c.stages[s].theta;
+        off[s] = g;
+        for (const sc::WeakLR &wk : c.stages[s].weak) {
+            std::copy(wk.w.begin(), wk.w.end(), w.begin() + (size_t)g * 36);
+            bias[g] = wk.bias;
+            std::copy(all.begin() + 4 * wk.patch_index, all.begin() + 4 * wk.patch_index + 4,
+                      d->patch_rects.begin() + 4 * g);
+            g++;
+        }
+    }
+    off[d->S] = g;
+    d->d_w.ensure(w.size());
+    d->d_bias.ensure(bias.size());
+    d->d_theta.ensure(theta.size());
+    d->d_stage_off.ensure(off.size());
+    HIPCHK(hipMemcpy(d->d_w.p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d->d_bias.p, bias.data(), bias.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d->d_theta.p, theta.data(), theta.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d->d_stage_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+}
+
+void check_params(const sc_scan_params &p) {
+    if (p.base_len < 1 || p.tmpl_w < 2 || p.tmpl_h < 2 || p.aspect_h < 1 ||
+        !(p.scale_factor > 1.0) || p.step < 0)
+        throw Error{SC_ERR_INVALID, "invalid scan parameters"};
+}
+
+sc_detector *make_detector(const sc::Cascade &c, const sc_scan_params *p, int device) {
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev)
+        throw Error{SC_ERR_DEVICE, "device " + std::to_string(device) + " not present (" +
+                                       std::to_string(ndev) + " visible)"};
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        throw Error{SC_ERR_DEVICE, std::string("kernels are built for gfx950, device is ") +
+                                       prop.gcnArchName};
+    HIPCHK(hipSetDevice(device));
+    auto *d = new sc_detector();
+    try {
+        d->device = device;
+        if (p) d->prm = *p;
+        else sc_scan_params_default(&d->prm);
+        check_params(d->prm);
+        d->casc = c;
+        HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        upload_model(d);
+    } catch (...) {
+        delete d;
+        throw;
+    }
+    return d;
+}
+
+void ensure_buffers(sc_detector *d, int n) {
+    const Geometry &g = d->geo;
+    const size_t frame_floats = (size_t)(g.H + 1) * g.pitch_cells * 8;
+    d->d_table.ensure(frame_floats * n);
+    d->d_counters.ensure((size_t)n + 1);
+    d->d_visited.ensure(1);
+    if (d->debug) {
+        d->d_dbg_p.ensure((size_t)g.grid * n);
+        d->d_dbg_s.ensure((size_t)g.grid * n);
+        d->d_dbg_v.ensure((size_t)g.grid * n);
+    }
+}
+
+void timed_begin(sc_detector *d, hipEvent_t *a) {
+    if (!d->timing) return;
+    *a = d->ev();
+    HIPCHK(hipEventRecord(*a, d->stream));
+}
+void timed_end(sc_detector *d, int kind, hipEvent_t a) {
+    if (!d->timing) return;
+    hipEvent_t b = d->ev();
+    HIPCHK(hipEventRecord(b, d->stream));
+    d->pending.push_back({kind, a, b});
+}
+
+// rowscan -> colscan -> windows on the detector's stream.
+void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int stride,
+             sc_det_record *d_out, int capacity, int *d_counts) {
+    build_geometry(d, W, H);
+    ensure_buffers(d, n);
+    const Geometry &g = d->geo;
+    const long long frame_floats = (long long)(g.H + 1) * g.pitch_cells * 8;
+    const int pitch = g.pitch_cells * 8;
+    HIPCHK(hipMemsetAsync(d_counts, 0, sizeof(int) * (n + 1), d->stream));
+    HIPCHK(hipMemsetAsync(d->d_visited.p, 0, sizeof(unsigned long long), d->stream));
+
+    sc::RowScanArgs ra{d_frames, (long long)H * stride, stride, W, H, d->d_table.p, frame_floats, pitch};
+    hipEvent_t e0 = nullptr;
+    timed_begin(d, &e0);
+    sc::launch_rowscan(ra, n, d->stream);
+    HIPCHK(hipGetLastError());
+    timed_end(d, SC_KERNEL_ROWSCAN, e0);
+
+    timed_begin(d, &e0);
+    sc::launch_colscan(d->d_table.p, frame_floats, pitch, W, H, n, d->stream);
+    HIPCHK(hipGetLastError());
+    timed_end(d, SC_KERNEL_COLSCAN, e0);
+
+    sc::WindowArgs wa{};
+    wa.table = d->d_table.p;
+    wa.frame_stride = frame_floats;
+    wa.pitch = pitch;
+    wa.rows = d->d_rows.p;
+    wa.levels = d->d_levels.p;
+    wa.proj = d->d_proj.p;
+    wa.w = reinterpret_cast<const float4 *>(d->d_w.p);
+    wa.bias = d->d_bias.p;
+    wa.theta = d->d_theta.p;
+    wa.stage_off = d->d_stage_off.p;
+    wa.K = d->K;
+    wa.n_stages = d->S;
+    wa.step = g.step;
+    wa.stride_score = d->prm.stride_score;
+    wa.out = d_out;
+    wa.capacity = capacity;
+    wa.counters = d_counts;
+    wa.visited = d->d_visited.p;
+    if (d->debug) {
+        wa.dbg_p = d->d_dbg_p.p;
+        wa.dbg_s = d->d_dbg_s.p;
+        wa.dbg_v = d->d_dbg_v.p;
+    }
+    wa.grid_per_frame = g.grid;
+    wa.lds_nx = (g.nx_max + 63) & ~63;
+    d->last_frames = n;
+    if (g.rows.empty()) return;
+    timed_begin(d, &e0);
+    sc::launch_windows(wa, (int)g.rows.size(), n, d->debug, d->stream);
+    HIPCHK(hipGetLastError());
+    timed_end(d, SC_KERNEL_WINDOWS, e0);
+    d->last_frames = n;
+}
+
+bool rec_less(const sc_det_record &a, const sc_det_record &b) {
+    if (a.frame != b.frame) return a.frame < b.frame;
+    if (a.level != b.level) return a.level < b.level;
+    if (a.y != b.y) return a.y < b.y;
+    return a.x < b.x;
+}
+
+// Synchronous device-frame detection with host output.
+int detect_device_sync(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int stride,
+                       sc_window *out, int capacity, int *n_out) {
+    if (n <= 0 || !d_frames || !n_out || (capacity > 0 && !out) || capacity < 0)
+        throw Error{SC_ERR_INVALID, "bad arguments"};
+    if (stride < W) throw Error{SC_ERR_INVALID, "stride smaller than width"};
+    size_t cap_dev = std::max<size_t>(d->d_out.n, 4096);
+    std::vector<int> counts(n + 1);
+    for (int attempt = 0; attempt < 2; attempt++) {
+        d->d_out.ensure(cap_dev);
+        d->d_counters.ensure((size_t)n + 1);
+        enqueue(d, d_frames, n, W, H, stride, d->d_out.p, (int)cap_dev, d->d_counters.p);
+        HIPCHK(hipMemcpyAsync(counts.data(), d->d_counters.p, sizeof(int) * (n + 1),
+                              hipMemcpyDeviceToHost, d->stream));
+        unsigned long long vis = 0;
+        HIPCHK(hipMemcpyAsync(&vis, d->d_visited.p, sizeof(vis), hipMemcpyDeviceToHost, d->stream));
+        HIPCHK(hipStreamSynchronize(d->stream));
+        d->last_visited = (long long)vis;
+        if ((size_t)counts[0] <= cap_dev) break;
+        cap_dev = (size_t)counts[0];
+    }
+    const int total = counts[0];
+    std::vector<sc_det_record> recs(total);
+    if (total > 0)
+        HIPCHK(hipMemcpy(recs.data(), d->d_out.p, sizeof(sc_det_record) * total, hipMemcpyDeviceToHost));
+    std::sort(recs.begin(), recs.end(), rec_less);
+    for (int f = 0; f < n; f++) n_out[f] = counts[1 + f];
+    const int m = std::min(total, capacity);
+    for (int i = 0; i < m; i++) {
+        const sc_det_record &r = recs[i];
+        out[i] = sc_window{r.level, r.x, r.y, r.w, r.h, r.stage_reached, r.score};
+    }
+    if (total > capacity) {
+        g_err = "output capacity " + std::to_string(capacity) + " < " + std::to_string(total);
+        return SC_ERR_CAPACITY;
+    }
+    return SC_OK;
+}
+
+template <class F>
+int guarded(F &&f) {
+    try {
+        return f();
+    } catch (const Error &e) {
+        return fail(e.code, e.msg);
+    } catch (const std::bad_alloc &) {
+        return fail(SC_ERR_NOMEM, "out of host memory");
+    } catch (const std::exception &e) {
+        return fail(SC_ERR_INVALID, e.what());
+    }
+}
+
+}  // namespace
+
+// =========================================================================
+// C ABI
+// =========================================================================
+extern "C" {
+
+void sc_scan_params_default(sc_scan_params *p) {
+    if (!p) return;
+    p->base_len = 70;
+    p->scale_factor = 1.1;
+    p->n_levels = -1;
+    p->step = 0;
+    p->prefilter_k = 6.0f;
+    p->stride_score = 0.5;
+    p->tmpl_w = 40;
+    p->tmpl_h = 40;
+    p->aspect_h = 1;
+}
+
+const char *sc_last_error(void) { return g_err.c_str(); }
+const char *sc_version(void) { return "surfcascade-mi355x 0.1 (gfx950)"; }
+
+int sc_model_parse(const char *text, size_t len, sc_model **out) {
+    return guarded([&] {
+        if (!text || !out) throw Error{SC_ERR_INVALID, "null argument"};
+        sc::CfgValue root = sc::cfg_parse(std::string(text, len));
+        auto *m = new sc_model{sc::cascade_from_cfg(root)};
+        *out = m;
+        return SC_OK;
+    });
+}
+
+int sc_model_load(const char *path, sc_model **out) {
+    return guarded([&] {
+        if (!path || !out) throw Error{SC_ERR_INVALID, "null argument"};
+        std::ifstream f(path, std::ios::binary);
+        if (!f) throw Error{SC_ERR_IO, std::string("I/O error while reading file: ") + path};
+        std::stringstream ss;
+        ss << f.rdbuf();
+        std::string t = ss.str();
+        sc::CfgValue root = sc::cfg_parse(t);
+        *out = new sc_model{sc::cascade_from_cfg(root)};
+        return SC_OK;
+    });
+}
+
+int sc_model_save(const sc_model *m, const char *path) {
+    return guarded([&] {
+        if (!m || !path) throw Error{SC_ERR_INVALID, "null argument"};
+        std::string t = sc::cfg_write(sc::cascade_to_cfg(m->c));
+        std::ofstream f(path, std::ios::binary);
+        if (!f) throw Error{SC_ERR_IO, std::string("I/O error while writing file: ") + path};
+        f << t;
+        if (!f) throw Error{SC_ERR_IO, std::string("I/O error while writing file: ") + path};
+        return SC_OK;
+    });
+}
+
+int sc_model_num_stages(const sc_model *m) { return m ? (int)m->c.stages.size() : SC_ERR_INVALID; }
+
+int sc_model_stage(const sc_model *m, int s, float *theta, int *n_weak) {
+    if (!m || s < 0 || s >= (int)m->c.stages.size()) return fail(SC_ERR_INVALID, "bad stage index");
+    if (theta) *theta = m->c.stages[s].theta;
+    if (n_weak) *n_weak = (int)m->c.stages[s].weak.size();
+    return SC_OK;
+}
+
+int sc_model_weak(const sc_model *m, int s, int k, int *patch_index, float w33[33], double *bias) {
+    if (!m || s < 0 || s >= (int)m->c.stages.size() || k < 0 ||
+        k >= (int)m->c.stages[s].weak.size())
+        return fail(SC_ERR_INVALID, "bad weak index");
+    const sc::WeakLR &wk = m->c.stages[s].weak[k];
+    if (patch_index) *patch_index = wk.patch_index;
+    if (bias) *bias = wk.bias;
+    if (w33)
+        for (int i = 0; i < 33; i++) w33[i] = i < (int)wk.w.size() ? wk.w[i] : 0.0f;
+    return SC_OK;
+}
+
+void sc_model_free(sc_model *m) { delete m; }
+
+int sc_extract_patches(int tw, int th, int32_t *rects, int cap) {
+    if (tw < 1 || th < 1) return fail(SC_ERR_INVALID, "bad template size");
+    std::vector<int32_t> r = sc::extract_patches(tw, th);
+    const int n = (int)r.size() / 4;
+    if (rects) std::copy(r.begin(), r.begin() + 4 * std::min(n, std::max(cap, 0)), rects);
+    return n;
+}
+
+int sc_detector_create_from_model(const sc_model *m, const sc_scan_params *p, int device,
+                                  sc_detector **out) {
+    return guarded([&] {
+        if (!m || !out) throw Error{SC_ERR_INVALID, "null argument"};
+        *out = make_detector(m->c, p, device);
+        return SC_OK;
+    });
+}
+
+int sc_detector_create(const char *path, const sc_scan_params *p, int device, sc_detector **out) {
+    sc_model *m = nullptr;
+    int rc = sc_model_load(path, &m);
+    if (rc != SC_OK) return rc;
+    rc = sc_detector_create_from_model(m, p, device, out);
+    sc_model_free(m);
+    return rc;
+}
+
+void sc_detector_destroy(sc_detector *d) { delete d; }
+
+void *sc_detector_stream(sc_detector *d) { return d ? (void *)d->stream : nullptr; }
+
+int sc_detect_device(sc_detector *d, const uint8_t *d_frames, int n, int w, int h, int stride,
+                     sc_window *out, int capacity, int *n_out) {
+    return guarded([&] {
+        if (!d) throw Error{SC_ERR_INVALID, "null detector"};
+        HIPCHK(hipSetDevice(d->device));
+        return detect_device_sync(d, d_frames, n, w, h, stride, out, capacity, n_out);
+    });
+}
+
+int sc_detect_batch(sc_detector *d, const uint8_t *const *frames, int n, int w, int h, int stride,
+                    sc_window *out, int capacity, int *n_out) {
+    return guarded([&] {
+        if (!d || !frames || n <= 0) throw Error{SC_ERR_INVALID, "bad arguments"};
+        if (w < 2 || h < 2 || stride < w) throw Error{SC_ERR_INVALID, "bad frame geometry"};
+        HIPCHK(hipSetDevice(d->device));
+        d->d_frames.ensure((size_t)w * h * n);
+        for (int f = 0; f < n; f++) {
+            if (!frames[f]) throw Error{SC_ERR_INVALID, "null frame pointer"};
+            HIPCHK(hipMemcpy2DAsync(d->d_frames.p + (size_t)w * h * f, w, frames[f], stride, w, h,
+                                    hipMemcpyHostToDevice, d->stream));
+        }
+        return detect_device_sync(d, d->d_frames.p, n, w, h, w, out, capacity, n_out);
+    });
+}
+
+int sc_detect(sc_detector *d, const uint8_t *gray, int w, int h, int stride, sc_window *out,
+              int capacity, int *n_out) {
+    const uint8_t *fr[1] = {gray};
+    return sc_detect_batch(d, fr, 1, w, h, stride, out, capacity, n_out);
+}
+
+int sc_enqueue_device(sc_detector *d, const uint8_t *d_frames, int n, int w, int h, int stride,
+                      sc_det_record *d_out, int capacity, int32_t *d_counts) {
+    return guarded([&] {
+        if (!d || !d_frames || n <= 0 || !d_counts || capacity < 0 || (capacity > 0 && !d_out))
+            throw Error{SC_ERR_INVALID, "bad arguments"};
+        if (w < 2 || h < 2 || stride < w) throw Error{SC_ERR_INVALID, "bad frame geometry"};
+        HIPCHK(hipSetDevice(d->device));
+        enqueue(d, d_frames, n, w, h, stride, d_out, capacity, d_counts);
+        return SC_OK;
+    });
+}
+
+int sc_synchronize(sc_detector *d) {
+    return guarded([&] {
+        if (!d) throw Error{SC_ERR_INVALID, "null detector"};
+        HIPCHK(hipStreamSynchronize(d->stream));
+        unsigned long long vis = 0;
+        HIPCHK(hipMemcpy(&vis, d->d_visited.p, sizeof(vis), hipMemcpyDeviceToHost));
+        d->last_visited = (long long)vis;
+        return SC_OK;
+    });
+}
+
+int sc_detector_info(sc_detector *d, int what, int64_t *value) {
+    if (!d || !value) return fail(SC_ERR_INVALID, "null argument");
+    switch (what) {
+        case SC_INFO_LEVELS: *value = d->geo.n_levels; break;
+        case SC_INFO_GRID_WINDOWS: *value = d->geo.grid; break;
+        case SC_INFO_ROWS: *value = (int64_t)d->geo.rows.size(); break;
+        case SC_INFO_TABLE_PITCH: *value = d->geo.pitch_cells; break;
+        case SC_INFO_VISITED: *value = d->last_visited; break;
+        default: return fail(SC_ERR_INVALID, "unknown info key");
+    }
+    return SC_OK;
+}
+
+int sc_detector_set_debug(sc_detector *d, int on) {
+    if (!d) return fail(SC_ERR_INVALID, "null detector");
+    d->debug = on != 0;
+    return SC_OK;
+}
+
+int sc_debug_dump(sc_detector *d, int what, int frame, void *dst, size_t bytes) {
+    return guarded([&] {
+        if (!d || !dst) throw Error{SC_ERR_INVALID, "null argument"};
+        if (frame < 0 || frame >= d->last_frames) throw Error{SC_ERR_INVALID, "bad frame index"};
+        HIPCHK(hipSetDevice(d->device));
+        HIPCHK(hipStreamSynchronize(d->stream));
+        const Geometry &g = d->geo;
+        if (what == SC_DUMP_INTEGRAL) {
+            const size_t row = (size_t)(g.W + 1) * 32, need = row * (g.H + 1);
+            if (bytes < need) throw Error{SC_ERR_CAPACITY, "dump buffer too small"};
+            const float *src = d->d_table.p + (size_t)frame * (g.H + 1) * g.pitch_cells * 8;
+            HIPCHK(hipMemcpy2D(dst, row, src, (size_t)g.pitch_cells * 32, row, g.H + 1,
+                               hipMemcpyDeviceToHost));
+            return SC_OK;
+        }
+        if (!d->debug) throw Error{SC_ERR_INVALID, "debug records disabled (sc_detector_set_debug)"};
+        const size_t n = (size_t)g.grid;
+        if (what == SC_DUMP_GRID_STAGE) {
+            if (bytes < n * 2) throw Error{SC_ERR_CAPACITY, "dump buffer too small"};
+            HIPCHK(hipMemcpy(dst, d->d_dbg_p.p + n * frame, n * 2, hipMemcpyDeviceToHost));
+        } else if (what == SC_DUMP_GRID_SCORE) {
+            if (bytes < n * 4) throw Error{SC_ERR_CAPACITY, "dump buffer too small"};
+            HIPCHK(hipMemcpy(dst, d->d_dbg_s.p + n * frame, n * 4, hipMemcpyDeviceToHost));
+        } else if (what == SC_DUMP_GRID_VISIT) {
+            if (bytes < n) throw Error{SC_ERR_CAPACITY, "dump buffer too small"};
+            HIPCHK(hipMemcpy(dst, d->d_dbg_v.p + n * frame, n, hipMemcpyDeviceToHost));
+        } else {
+            throw Error{SC_ERR_INVALID, "unknown dump kind"};
+        }
+        return SC_OK;
+    });
+}
+
+int sc_set_timing(sc_detector *d, int on) {
+    if (!d) return fail(SC_ERR_INVALID, "null detector");
+    d->timing = on != 0;
+    return SC_OK;
+}
+
+int sc_get_timing(sc_detector *d, double ms[SC_KERNEL_COUNT], int64_t n[SC_KERNEL_COUNT]) {
+    return guarded([&] {
+        if (!d) throw Error{SC_ERR_INVALID, "null detector"};
+        HIPCHK(hipStreamSynchronize(d->stream));
+        for (auto &p : d->pending) {
+            float t = 0;
+            HIPCHK(hipEventElapsedTime(&t, p.a, p.b));
+            d->t_ms[p.kind] += t;
+            d->t_n[p.kind] += 1;
+            d->event_pool.push_back(p.a);
+            d->event_pool.push_back(p.b);
+        }
+        d->pending.clear();
+        for (int k = 0; k < SC_KERNEL_COUNT; k++) {
+            if (ms) ms[k] = d->t_ms[k];
+            if (n) n[k] = d->t_n[k];
+            d->t_ms[k] = 0;
+            d->t_n[k] = 0;
+        }
+        return SC_OK;
+    });
+}
+
+}  // extern "C"

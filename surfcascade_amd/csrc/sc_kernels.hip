@@ -1,0 +1,476 @@
+// sc_kernels.hip -- gfx950 (CDNA4) kernels of the SURF-cascade detect path.
+//
+//   rowscan  : T2bFilter gradients (DenseSURFFeatureExtractor.cpp:199-349)
+//              fused with the exact integer row prefix of cv::integral
+//              (:73-76); writes R_y[x] (exact in f32) into the table rows.
+//   colscan  : the f32 column recurrence S[y+1][x] = S[y][x] + R_y[x],
+//              sequential in y per (x, channel) -- the association order of
+//              OpenCV's scalar integral_; table layout = F256Dat interleave
+//              (.h:21-25, merge :80).
+//   windows  : one workgroup per (frame, level, row y): prefilter
+//              (sum(), :351-358 / ObjDetector.cpp:188), then the cascade
+//              stage by stage over a compacted survivor list (ballot +
+//              prefix), (window, weak) items spread over all lanes; each item
+//              is ProjectPatches/CalcFeature/Normalize/LogisticRegression::
+//              Predict (:459-484, :379-457, LogisticRegression.cpp:46-68);
+//              stage sums in weak order (GentleAdaboost.cpp:247-261); finally
+//              the adaptive-stride x walk of ObjDetector.cpp:185-217 over
+//              the row's results, emitting detections.
+//
+// Every f32/f64 operation is the one the reference performs, in its order;
+// the file is compiled with -ffp-contract=off (no FMA contraction), IEEE
+// sqrt / division (hipcc default), no fast-math.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+#include "sc_kernels.hpp"
+
+namespace sc {
+
+namespace {
+
+constexpr int kRowThreads = 256;
+constexpr int kRowSeg = kRowThreads * 8;  // pixels per rowscan segment
+constexpr int kWinThreads = 256;
+constexpr int kWaves = kWinThreads / 64;
+
+__device__ __forceinline__ uint32_t sat_sub(uint32_t a, uint32_t b) { return a > b ? a - b : 0u; }
+
+// ---------------------------------------------------------------------------
+// rowscan: gradients + exact integer row prefix -> table rows 1..H
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kRowThreads) void rowscan_kernel(RowScanArgs a) {
+    __shared__ uint8_t s_img[3][kRowSeg + 16];
+    __shared__ uint32_t s_wsum[kRowThreads / 64][8];
+
+    const int y = blockIdx.x, frame = blockIdx.y, tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    const int W = a.W, H = a.H;
+    const uint8_t *img = a.frames + (long long)frame * a.frame_bytes;
+    const uint8_t *rows[3] = {img + (long long)(y > 0 ? y - 1 : 0) * a.stride,
+                              img + (long long)y * a.stride,
+                              img + (long long)(y < H - 1 ? y + 1 : H - 1) * a.stride};
+    float *tab = a.table + (long long)frame * a.frame_stride;
+    float *out = tab + (long long)(y + 1) * a.pitch;
+
+    if (y == 0)  // table row 0 is all zeros
+        for (int i = tid; i < a.pitch; i += kRowThreads) tab[i] = 0.0f;
+    if (tid < 8) out[tid] = 0.0f;  // column 0
+
+    uint32_t carry[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) carry[c] = 0;
+
+    for (int seg = 0; seg < W; seg += kRowSeg) {
+        // stage the three source rows of this segment (x = seg-1 .. seg+2048)
+        for (int i = tid; i < kRowSeg + 2; i += kRowThreads) {
+            int x = seg - 1 + i;
+            x = x < 0 ? 0 : (x > W - 1 ? W - 1 : x);
+#pragma unroll
+            for (int r = 0; r < 3; r++) s_img[r][i] = rows[r][x];
+        }
+        __syncthreads();
+
+        const int x0 = seg + tid * 8;
+        uint32_t pre[8][8];  // inclusive in-thread prefix [px][ch]
+        uint32_t acc[8];
+#pragma unroll
+        for (int c = 0; c < 8; c++) acc[c] = 0;
+#pragma unroll
+        for (int px = 0; px < 8; px++) {
+            const int x = x0 + px;
+            if (x < W) {
+                const int xn = (x < W - 1 ? x + 1 : W - 1) - seg + 1;
+                const int xp = (x > 0 ? x - 1 : 0) - seg + 1;
+                const int xc = x - seg + 1;
+                const uint32_t u_c = s_img[0][xc], d_c = s_img[2][xc];
+                const uint32_t c_n = s_img[1][xn], c_p = s_img[1][xp];
+                const uint32_t u_n = s_img[0][xn], u_p = s_img[0][xp];
+                const uint32_t d_n = s_img[2][xn], d_p = s_img[2][xp];
+                acc[0] += sat_sub(c_p, c_n);  // dx: In = I[y][x+1], Ip = I[y][x-1]
+                acc[1] += sat_sub(c_n, c_p);
+                acc[2] += sat_sub(u_c, d_c);  // dy: In = I[y+1][x], Ip = I[y-1][x]
+                acc[3] += sat_sub(d_c, u_c);
+                acc[4] += sat_sub(u_p, d_n);  // du: In = I[y+1][x+1], Ip = I[y-1][x-1]
+                acc[5] += sat_sub(d_n, u_p);
+                acc[6] += sat_sub(d_p, u_n);  // dv: In = I[y-1][x+1], Ip = I[y+1][x-1]
+                acc[7] += sat_sub(u_n, d_p);
+            }
+#pragma unroll
+            for (int c = 0; c < 8; c++) pre[px][c] = acc[c];
+        }
+        // exclusive scan of the per-thread totals across the workgroup (exact ints)
+        uint32_t incl[8];
+#pragma unroll
+        for (int c = 0; c < 8; c++) incl[c] = acc[c];
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                uint32_t v = __shfl_up(incl[c], off, 64);
+                if (lane >= off) incl[c] += v;
+            }
+        }
+        if (lane == 63)
+#pragma unroll
+            for (int c = 0; c < 8; c++) s_wsum[wv][c] = incl[c];
+        __syncthreads();
+        uint32_t base[8], seg_total[8];
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            uint32_t b = 0, t = 0;
+            for (int w = 0; w < kRowThreads / 64; w++) {
+                if (w < wv) b += s_wsum[w][c];
+                t += s_wsum[w][c];
+            }
+            base[c] = carry[c] + b + incl[c] - acc[c];
+            seg_total[c] = t;
+        }
+#pragma unroll
+        for (int px = 0; px < 8; px++) {
+            const int x = x0 + px;
+            if (x < W) {
+                float4 lo, hi;
+                lo.x = (float)(base[0] + pre[px][0]);
+                lo.y = (float)(base[1] + pre[px][1]);
+                lo.z = (float)(base[2] + pre[px][2]);
+                lo.w = (float)(base[3] + pre[px][3]);
+                hi.x = (float)(base[4] + pre[px][4]);
+                hi.y = (float)(base[5] + pre[px][5]);
+                hi.z = (float)(base[6] + pre[px][6]);
+                hi.w = (float)(base[7] + pre[px][7]);
+                float4 *dst = reinterpret_cast<float4 *>(out + (long long)(x + 1) * 8);
+                dst[0] = lo;
+                dst[1] = hi;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 8; c++) carry[c] += seg_total[c];
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// colscan: S[y+1][x] = fl(S[y][x] + R_y[x]), sequential in y (in place)
+// ---------------------------------------------------------------------------
+constexpr int kColBlk = 32;
+
+__global__ __launch_bounds__(64) void colscan_kernel(float *table, long long frame_stride,
+                                                     int pitch, int W, int H) {
+    const int idx = blockIdx.x * 64 + threadIdx.x;
+    if (idx >= (W + 1) * 8) return;
+    float *col = table + (long long)blockIdx.y * frame_stride + idx;
+    float acc = 0.0f;  // row 0
+    float cur[kColBlk], nxt[kColBlk];
+#pragma unroll
+    for (int k = 0; k < kColBlk; k++) cur[k] = (1 + k <= H) ? col[(long long)(1 + k) * pitch] : 0.0f;
+    for (int y = 1; y <= H; y += kColBlk) {
+        const int yn = y + kColBlk;
+#pragma unroll
+        for (int k = 0; k < kColBlk; k++)
+            nxt[k] = (yn + k <= H) ? col[(long long)(yn + k) * pitch] : 0.0f;
+#pragma unroll
+        for (int k = 0; k < kColBlk; k++) {
+            if (y + k <= H) {
+                acc = acc + cur[k];
+                col[(long long)(y + k) * pitch] = acc;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kColBlk; k++) cur[k] = nxt[k];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// windows
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
+
+// (TL + BR) - (TR + BL) per lane (DenseSURFFeatureExtractor.cpp:385-412).
+__device__ __forceinline__ float4 box4(float4 tl, float4 br, float4 tr, float4 bl) {
+    float4 r;
+    r.x = (tl.x + br.x) - (tr.x + bl.x);
+    r.y = (tl.y + br.y) - (tr.y + bl.y);
+    r.z = (tl.z + br.z) - (tr.z + bl.z);
+    r.w = (tl.w + br.w) - (tr.w + bl.w);
+    return r;
+}
+
+// sum(win) > area*k  (DenseSURFFeatureExtractor.cpp:351-358, ObjDetector.cpp:188)
+__device__ __forceinline__ bool prefilter(const float *T, int pitch, int x, int y, int w, int h,
+                                          float thr) {
+    const float *r0 = T + (long long)y * pitch, *r1 = T + (long long)(y + h) * pitch;
+    float4 v = box4(ld4(r0 + x * 8), ld4(r1 + (x + w) * 8), ld4(r0 + (x + w) * 8), ld4(r1 + x * 8));
+    float m = (((v.x + v.y) + v.z) + v.w) / 2.0f;
+    return m > thr;
+}
+
+// c_k = (q0+q1)+(q2+q3); SS = (((eps + c0) + c1) ...) + c7   (:427-433)
+__device__ __forceinline__ float ss_hadd(const float (&f)[32]) {
+    float ss = FLT_EPSILON;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        float q0 = f[4 * k] * f[4 * k], q1 = f[4 * k + 1] * f[4 * k + 1];
+        float q2 = f[4 * k + 2] * f[4 * k + 2], q3 = f[4 * k + 3] * f[4 * k + 3];
+        ss = ss + ((q0 + q1) + (q2 + q3));
+    }
+    return ss;
+}
+
+// One (window, weak classifier) item: CalcFeature + Normalize + Predict.
+__device__ float weak_eval(const float *T, int pitch, int X, int Y, ProjPatch pj,
+                           const float4 *__restrict__ w4, double bias) {
+    const int x0 = X + pj.dx, y0 = Y + pj.dy, c = pj.c;
+    const int gw = pj.shape == 1 ? 1 : (pj.shape == 2 ? 4 : 2);
+    float f[32];
+#pragma unroll
+    for (int cell = 0; cell < 4; cell++) {
+        const int cx = cell % gw, cy = cell / gw;
+        const int xa = x0 + cx * c, ya = y0 + cy * c;
+        const float *ra = T + (long long)ya * pitch, *rb = T + (long long)(ya + c) * pitch;
+        const float *tl = ra + xa * 8, *tr = ra + (xa + c) * 8;
+        const float *bl = rb + xa * 8, *br = rb + (xa + c) * 8;
+        float4 lo = box4(ld4(tl), ld4(br), ld4(tr), ld4(bl));
+        float4 hi = box4(ld4(tl + 4), ld4(br + 4), ld4(tr + 4), ld4(bl + 4));
+        f[8 * cell + 0] = lo.x; f[8 * cell + 1] = lo.y; f[8 * cell + 2] = lo.z; f[8 * cell + 3] = lo.w;
+        f[8 * cell + 4] = hi.x; f[8 * cell + 5] = hi.y; f[8 * cell + 6] = hi.z; f[8 * cell + 7] = hi.w;
+    }
+    // Normalize (:417-457): clip at sqrt(SS)*theta, renormalise by 1/sqrt(SS2)
+    const float theta = 0.35355338f;  // 2/sqrt(32.f) (.h:36)
+    const float t = sqrtf(ss_hadd(f)) * theta, nt = -t;
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+        float v = f[i] < t ? f[i] : t;  // _mm_min_ps
+        f[i] = v > nt ? v : nt;         // _mm_max_ps
+    }
+    const float r = 1.0f / sqrtf(ss_hadd(f));
+#pragma unroll
+    for (int i = 0; i < 32; i++) f[i] = f[i] * r;
+    // LogisticRegression::Predict (LogisticRegression.cpp:46-68)
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const float4 wv = w4[i];
+        s0 = wv.x * f[4 * i + 0] + s0;
+        s1 = wv.y * f[4 * i + 1] + s1;
+        s2 = wv.z * f[4 * i + 2] + s2;
+        s3 = wv.w * f[4 * i + 3] + s3;
+    }
+    const float z32 = (s0 + s1) + (s2 + s3);
+    double prob = (double)z32;
+    prob += (double)w4[8].x * bias;
+    prob = 1.0 / (1.0 + exp(-prob));
+    return (float)prob;
+}
+
+struct WinSmem {
+    int *cnt;  // [kWaves]
+    float *st_s;
+    float *sums;
+    int16_t *st_p;
+    uint16_t *surv;
+    float *P;  // [kWinThreads]
+};
+
+__device__ __forceinline__ WinSmem carve(unsigned char *smem, int nxa) {
+    WinSmem m;
+    m.cnt = reinterpret_cast<int *>(smem);
+    m.st_s = reinterpret_cast<float *>(smem + 16);
+    m.sums = m.st_s + nxa;
+    m.P = m.sums + nxa;
+    m.st_p = reinterpret_cast<int16_t *>(m.P + kWinThreads);
+    m.surv = reinterpret_cast<uint16_t *>(m.st_p + nxa);
+    return m;
+}
+
+// Order-preserving block compaction: appends j to surv when keep.
+__device__ __forceinline__ int compact_append(bool keep, int j, uint16_t *surv, int n, int *cnt) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(keep);
+    const int pre = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) cnt[wv] = __popcll(m);
+    __syncthreads();
+    int off = n, total = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) {
+        const int cw = cnt[w];
+        if (w < wv) off += cw;
+        total += cw;
+    }
+    if (keep) surv[off + pre] = (uint16_t)j;
+    __syncthreads();
+    return n + total;
+}
+
+template <bool kDebug>
+__global__ __launch_bounds__(kWinThreads) void window_kernel(WindowArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int row = blockIdx.x, frame = blockIdx.y;
+    const int2 rd = a.rows[row];
+    const LevelInfo L = a.levels[rd.x];
+    const int y = rd.y, nx = L.nx, step = a.step;
+    const int nxa = a.lds_nx;
+    WinSmem sm = carve(smem, nxa);
+    const float *T = a.table + (long long)frame * a.frame_stride;
+    const int pitch = a.pitch;
+
+    // 1) prefilter over the whole row; survivors in x order
+    int nsurv = 0;
+    for (int b = 0; b < nx; b += kWinThreads) {
+        const int j = b + tid;
+        bool pass = false;
+        if (j < nx) {
+            pass = prefilter(T, pitch, j * step, y, L.l, L.lh, L.thr);
+            sm.st_p[j] = pass ? 0 : -1;
+            sm.st_s[j] = 0.0f;
+        }
+        nsurv = compact_append(pass, j, sm.surv, nsurv, sm.cnt);
+    }
+
+    // 2) cascade, stage by stage over the compacted survivors
+    const ProjPatch *projL = a.proj + (long long)rd.x * a.K;
+    for (int s = 0; s < a.n_stages && nsurv > 0; s++) {
+        const int off = a.stage_off[s], n = a.stage_off[s + 1] - off;
+        for (int i = tid; i < nsurv; i += kWinThreads) sm.sums[i] = 0.0f;
+        __syncthreads();
+        const int items = nsurv * n;
+        for (int r = 0; r < items; r += kWinThreads) {
+            const int t = r + tid;
+            if (t < items) {
+                const int k = t / nsurv, i = t - k * nsurv;
+                const int j = sm.surv[i];
+                const int g = off + k;
+                sm.P[tid] = weak_eval(T, pitch, j * step, y, projL[g], a.w + (long long)g * 9, a.bias[g]);
+            }
+            __syncthreads();
+            const int rend = min(r + kWinThreads, items);
+            for (int i = tid; i < nsurv; i += kWinThreads) {
+                // items of slot i in [r, rend): t = k*nsurv + i, in increasing k
+                int k = (r > i) ? (r - i + nsurv - 1) / nsurv : 0;
+                float acc = sm.sums[i];
+                for (int t2 = k * nsurv + i; t2 < rend; t2 += nsurv) acc += sm.P[t2 - r];
+                sm.sums[i] = acc;
+            }
+            __syncthreads();
+        }
+        // stage decision (GentleAdaboost.cpp:259; ObjDetector.cpp:197)
+        const float th = a.theta[s];
+        int nn = 0;
+        for (int b = 0; b < nsurv; b += kWinThreads) {
+            const int i = b + tid;
+            bool keep = false;
+            int j = 0;
+            if (i < nsurv) {
+                j = sm.surv[i];
+                const float sc = sm.sums[i] / (float)n;
+                sm.st_s[j] = sc;
+                keep = !((double)sc < (double)th);
+                sm.st_p[j] = (int16_t)(keep ? s + 1 : s);
+            }
+            nn = compact_append(keep, j, sm.surv, nn, sm.cnt);
+        }
+        nsurv = nn;
+    }
+    __syncthreads();
+
+    // 3) adaptive-stride walk of the row (ObjDetector.cpp:185-217) by wave 0
+    if (tid < 64) {
+        const int S = a.n_stages;
+        const long long gbase = L.grid_base + (long long)(y / step) * nx;
+        int start = 0;
+        unsigned long long nvis = 0;
+        for (int b = 0; b < nx; b += 64) {
+            const int j = b + lane;
+            bool skip = true, det = false;
+            int p = -1;
+            float sl = 0.0f;
+            double fin = 0.0;
+            if (j < nx) {
+                p = sm.st_p[j];
+                sl = sm.st_s[j];
+                if (p >= 0) {
+                    fin = ((double)sl + p + 1) / S;  // ObjDetector.cpp:201
+                    skip = fin < a.stride_score;     // :214
+                    det = p == S;                    // :203
+                }
+            }
+            const unsigned long long sk = __ballot(skip);
+            const int lim = min(64, nx - b);
+            unsigned long long vis = 0;
+            int pos = start;
+            while (pos < lim) {
+                vis |= 1ull << pos;
+                pos += ((sk >> pos) & 1ull) ? 2 : 1;
+            }
+            start = pos - 64;
+            const bool v = (vis >> lane) & 1ull;
+            nvis += __popcll(vis);
+            if (kDebug && j < nx) {
+                const long long gi = (long long)frame * a.grid_per_frame + gbase + j;
+                a.dbg_p[gi] = (int16_t)p;
+                a.dbg_s[gi] = sl;
+                a.dbg_v[gi] = v ? 1 : 0;
+            }
+            const bool d = v && det;
+            const unsigned long long dm = __ballot(d);
+            if (dm) {
+                const int cnt = __popcll(dm);
+                int slot0 = 0;
+                if (lane == 0) {
+                    slot0 = atomicAdd(&a.counters[0], cnt);
+                    atomicAdd(&a.counters[1 + frame], cnt);
+                }
+                slot0 = __shfl(slot0, 0, 64);
+                if (d) {
+                    const int idx = slot0 + __popcll(dm & ((1ull << lane) - 1ull));
+                    if (idx < a.capacity) {
+                        sc_det_record rec;
+                        rec.frame = frame;
+                        rec.level = rd.x;
+                        rec.x = j * step;
+                        rec.y = y;
+                        rec.w = L.l;
+                        rec.h = L.lh;
+                        rec.stage_reached = p;
+                        rec._pad = 0;
+                        rec.score = fin;
+                        a.out[idx] = rec;
+                    }
+                }
+            }
+        }
+        if (lane == 0 && a.visited) atomicAdd(a.visited, nvis);
+    }
+}
+
+}  // namespace
+
+void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
+    hipLaunchKernelGGL(rowscan_kernel, dim3(a.H, n_frames), dim3(kRowThreads), 0, s, a);
+}
+
+void launch_colscan(float *table, long long frame_stride, int pitch, int W, int H, int n_frames,
+                    hipStream_t s) {
+    const int n = (W + 1) * 8;
+    hipLaunchKernelGGL(colscan_kernel, dim3((n + 63) / 64, n_frames), dim3(64), 0, s, table,
+                       frame_stride, pitch, W, H);
+}
+
+size_t window_lds_bytes(int nx_max) {
+    const int nxa = (nx_max + 63) & ~63;
+    return 16 + (size_t)nxa * 4 * 2 + kWinThreads * 4 + (size_t)nxa * 2 * 2;
+}
+
+void launch_windows(const WindowArgs &a, int n_rows, int n_frames, bool debug, hipStream_t s) {
+    const size_t lds = window_lds_bytes(a.lds_nx);
+    if (debug)
+        hipLaunchKernelGGL(window_kernel<true>, dim3(n_rows, n_frames), dim3(kWinThreads), lds, s, a);
+    else
+        hipLaunchKernelGGL(window_kernel<false>, dim3(n_rows, n_frames), dim3(kWinThreads), lds, s, a);
+}
+
+}  // namespace sc

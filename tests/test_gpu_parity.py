@@ -1,0 +1,152 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU restatement.
+
+Bit-exact: integral tables, per-window stage reached, per-window last stage
+score (f32 bits), visited set and detection windows; detection scores
+(f64) compared exactly as well (tolerance stated by north_star: 1e-5, the
+test demands equality and reports the max |diff| if it ever fails).
+"""
+import numpy as np
+import pytest
+
+from conftest import FACE_CFG, PED_CFG
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sc():
+    import surfcascade_amd as sc
+    return sc
+
+
+def _frame(W, H, seed):
+    from surfcascade_amd import synth
+    return synth.make_frame(W, H, seed)
+
+
+def _det_set(arr):
+    return sorted((int(r["level"]), int(r["y"]), int(r["x"]), int(r["w"]), int(r["h"]),
+                   int(r["stage"]), float(r["score"])) for r in arr)
+
+
+@pytest.mark.parametrize("W,H,seed", [(640, 480, 1), (1920, 1080, 1000), (257, 131, 7), (2, 2, 3),
+                                      (3000, 67, 5)])
+def test_integral_bit_exact(sc, oracle, W, H, seed):
+    img = _frame(W, H, seed)
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1))
+    det.detect(img)  # frames smaller than the window: no rows, integral still built
+    T = det.dump_integral(W, H)
+    ref = oracle.integral(img)
+    assert T.view(np.uint32).tobytes() == ref.view(np.uint32).tobytes()
+
+
+def _grid_parity(sc, oracle, cascade, cfg, img, params_sc, params_or):
+    det = sc.Detector(cfg, params_sc)
+    det.set_debug(True)
+    wins = det.detect(img)
+    p, s, v = det.dump_grid()
+    T = oracle.integral(img)
+    rp, rs = oracle.eval_grid(T, cascade, params_or)
+    assert len(p) == len(rp)
+    np.testing.assert_array_equal(p, rp)
+    assert s.view(np.uint32).tobytes() == rs.view(np.uint32).tobytes()
+    H, W = img.shape
+    layout, _ = oracle.grid_layout(W, H, params_or)
+    rv, rdm = oracle.walk_rows(rp, rs, layout, cascade.n_stages, params_or.stride_score)
+    np.testing.assert_array_equal(v, rv)
+    ref, nvis = oracle.detect(T, cascade, params_or)
+    assert det.info("visited") == nvis == int(rv.sum())
+    assert _det_set(wins) == _det_set(ref)
+    return wins, p
+
+
+def test_grid_parity_640x480_single_scale(sc, oracle, face_cascade):
+    img = _frame(640, 480, 1)
+    _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=1),
+                 oracle.Params(n_levels=1))
+
+
+def test_grid_parity_1080p_24_levels(sc, oracle, face_cascade):
+    img = _frame(1920, 1080, 1000)
+    _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=24),
+                 oracle.Params(n_levels=24))
+
+
+def test_grid_parity_default_levels_odd_size(sc, oracle, face_cascade):
+    img = _frame(803, 611, 11)
+    _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(), oracle.Params())
+
+
+def test_pedestrian_64x128(sc, oracle, ped_cascade):
+    img = _frame(960, 540, 21)
+    _grid_parity(sc, oracle, ped_cascade, PED_CFG, img,
+                 sc.ScanParams.pedestrian(n_levels=12),
+                 oracle.Params(base_len=64, aspect_h=2, n_levels=12))
+
+
+def test_permissive_cascade_many_detections(sc, oracle, face_cascade):
+    """Lowered thetas: many windows reach the last stage (detections + stride 1)."""
+    from surfcascade_amd import synth
+    c = face_cascade
+    theta = np.full(c.n_stages, 0.2, np.float32)
+    tree = synth.cascade_tree(c.n_weak, theta, c.patch_index, c.w, c.bias)
+    text = synth.write_cfg(tree)
+    casc_sc = sc.Model.parse(text)
+    casc_or = oracle.cascade_from_cfg(text)
+    img = _frame(640, 480, 2)
+    det = sc.Detector(casc_sc, sc.ScanParams(n_levels=3))
+    wins = det.detect(img)
+    T = oracle.integral(img)
+    ref, nvis = oracle.detect(T, casc_or, oracle.Params(n_levels=3))
+    assert len(ref) > 100
+    assert _det_set(wins) == _det_set(ref)
+    assert det.info("visited") == nvis
+
+
+def test_batch_equals_single(sc, oracle, face_cascade):
+    frames = np.stack([_frame(640, 480, 100 + k) for k in range(4)])
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=5))
+    batch = det.detect_batch(frames)
+    for k in range(4):
+        single = det.detect(frames[k])
+        assert _det_set(single) == _det_set(batch[k])
+        T = oracle.integral(frames[k])
+        ref, _ = oracle.detect(T, face_cascade, oracle.Params(n_levels=5))
+        assert _det_set(single) == _det_set(ref)
+
+
+def test_constant_image_no_windows(sc):
+    """KAT 4: constant image -> zero gradients -> prefilter fails everywhere."""
+    img = np.full((300, 400), 77, np.uint8)
+    det = sc.Detector(FACE_CFG, sc.ScanParams())
+    det.set_debug(True)
+    assert len(det.detect(img)) == 0
+    p, s, v = det.dump_grid()
+    assert (p == -1).all()
+    # every row walked at stride 2*step: visited = ceil(nx/2) per row
+    assert det.info("visited") == int(v.sum())
+
+
+def test_device_resident_frames(sc, oracle, face_cascade):
+    import torch
+    frames = np.stack([_frame(640, 480, 300 + k) for k in range(2)])
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=4))
+    dev = torch.from_numpy(frames).to("cuda:0")
+    res = det.detect_device(dev)
+    for k in range(2):
+        T = oracle.integral(frames[k])
+        ref, _ = oracle.detect(T, face_cascade, oracle.Params(n_levels=4))
+        assert _det_set(res[k]) == _det_set(ref)
+
+
+def test_capacity_error_reports_count(sc):
+    from surfcascade_amd import synth
+    from oracle import oracle as O
+    oc = O.cascade_from_cfg(open(FACE_CFG).read())
+    text = synth.write_cfg(synth.cascade_tree(oc.n_weak, np.zeros(oc.n_stages, np.float32),
+                                              oc.patch_index, oc.w, oc.bias))
+    det = sc.Detector(sc.Model.parse(text), sc.ScanParams(n_levels=1))
+    img = _frame(640, 480, 1)
+    with pytest.raises(sc.SurfCascadeError) as e:
+        det.detect(img, capacity=3)
+    assert e.value.code == -6
