@@ -1,0 +1,200 @@
+"""Benchmark: detection windows/s on the 1080p 24-level pyramid (BASELINE.json
+metric, config C2 on one GPU; C3-style frame sharding for --gpus N).
+
+A step = one pass of the detect path over one batch of synthetic 1080p frames
+already resident in HBM: gradient+integral (rowscan, colscan), prefilter +
+cascade + adaptive-stride walk (windows), and the gather of the raw detection
+records (RCCL all_gather when N > 1).  value = stride-3 grid windows of all
+frames of all ranks / max-over-ranks wall time.  Prints one JSON line (rank 0).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16, help="1080p frames per GPU per step")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--levels", type=int, default=24)
+    ap.add_argument("--model", default=os.path.join(ROOT, "surfcascade_amd", "models", "face40_synth.cfg"))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(frames, model_path, levels, seconds):
+    """The CPU restatement (oracle/, OpenMP over levels like ObjDetector.cpp:177)
+    on a bounded sample of the same frames: in-memory u8 frame -> raw detections."""
+    from oracle import oracle as O
+    O.build()
+    casc = O.cascade_from_cfg(open(model_path).read())
+    params = O.Params(n_levels=levels)
+    H, W = frames.shape[1:]
+    grid = O.grid_count(W, H, params)
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    threads = max(1, min(16, ncpu))
+    scratch = np.zeros((H + 1) * (W + 1) * 8, np.float32)
+    res = {}
+    for nt, budget in ((threads, seconds), (1, seconds)):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            O.detect_frame(frames[done % len(frames)], casc, params, nthreads=nt, scratch=scratch)
+            done += 1
+            if time.perf_counter() - t0 >= budget:
+                break
+        dt = time.perf_counter() - t0
+        res[nt] = (done * grid / dt, done, dt)
+    v, done, dt = res[threads]
+    v1, done1, dt1 = res[1]
+    return {"value": v, "unit": "windows/s", "cores": threads, "kind": "port",
+            "sample": "%d x %dx%d frames (%d levels, %d grid windows each), integral + adaptive-stride "
+                      "detect, %.1f s at %d threads; 1 thread: %.4g windows/s (%d frames, %.1f s)"
+                      % (done, W, H, levels, grid, dt, threads, v1, done1, dt1),
+            "value_1thread": v1}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+
+    import torch
+    import surfcascade_amd as sc
+    from surfcascade_amd import synth
+    from surfcascade_amd.dist import gather_detections, merge_records, shard_range
+
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    W, H, B = args.width, args.height, args.batch
+    # frame sharding: rank r owns frames 1000 + r*B .. (seeds) -- C3 layout
+    start, _ = shard_range(B * world, world, rank)
+    host_frames = synth.make_frames(W, H, B, seed0=1000 + start)
+    frames = torch.from_numpy(host_frames).to(f"cuda:{local_rank}")
+    params = sc.ScanParams(n_levels=args.levels)
+    det = sc.Detector(args.model, params, device=local_rank)
+    cap = 256 * B
+    recs = torch.zeros(cap * sc.RECORD_DTYPE.itemsize, dtype=torch.uint8, device=frames.device)
+    counts = torch.zeros(1 + B, dtype=torch.int32, device=frames.device)
+    gathered = {"counts": [counts], "recs": [recs]}
+
+    def step():
+        det.enqueue_device(frames, recs, counts)
+        det.synchronize()
+        if dist is not None:  # RCCL gather of the detection records (fixed-size pad)
+            gc, gr = gather_detections(counts, recs)
+            gathered["counts"], gathered["recs"] = gc, gr
+
+    for _ in range(args.warmup):
+        step()
+    grid = det.info("grid_windows")
+    det.get_timing()  # discard
+    det.set_timing(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    det.set_timing(False)
+    kt = det.get_timing()
+    visited = det.info("visited")
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=frames.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    merged = merge_records(gathered["counts"], gathered["recs"],
+                           [shard_range(B * world, world, r)[0] for r in range(world)])
+    total_det = len(merged)
+
+    if rank == 0:
+        windows = grid * B * args.steps * world
+        value = windows / dt
+        # roofline of the dominant kernel (windows): its compulsory bytes per
+        # launch = the integral table read once (32 B x (W+1)(H+1) per frame)
+        tab_bytes = 32 * (W + 1) * (H + 1)
+        ms_win, n_win = kt["windows"]
+        avg_win_s = ms_win / 1e3 / max(n_win, 1)
+        achieved = tab_bytes * B / avg_win_s / 1e9
+        # whole pipeline (SURVEY.md 8d per-unit figure: W*H + 64 (W+1)(H+1) per frame)
+        pipe_bytes = W * H + 64 * (W + 1) * (H + 1)
+        pipe_s = sum(v[0] for v in kt.values()) / 1e3 / max(n_win, 1)
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_windows.json")
+        if os.path.exists(pmc_path):
+            with open(pmc_path) as f:
+                pm = json.load(f)
+            if pm.get("batch") == B and pm.get("width") == W and pm.get("levels") == args.levels:
+                traffic = pm.get("hbm_bytes_per_launch")
+        line = {
+            "metric": "detection windows/sec on 1080p 24-scale pyramid",
+            "value": value,
+            "unit": "windows/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded 1080p frames, seeded 10-stage 40x40 cascade, thetas calibrated "
+                    "on held-out frames)",
+            "config": {"workload": "C2: %dx%d frames, %d-level window pyramid (l=70..%d), 40x40 face "
+                                   "cascade 10 stages / 190 weak LR; frame-sharded, %d frames per GPU "
+                                   "per step" % (W, H, args.levels,
+                                                  int(70 * 1.1 ** (args.levels - 1)), B),
+                       "frames_per_gpu_per_step": B, "grid_windows_per_frame": grid,
+                       "levels": args.levels, "parallelism": "frame-sharded dp%d" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "window_kernel", "avg_launch_ms": avg_win_s * 1e3,
+                         "bytes_per_launch": tab_bytes * B,
+                         "pipeline_achieved": pipe_bytes * B / pipe_s / 1e9,
+                         "pipeline_frac": pipe_bytes * B / pipe_s / 1e9 / HBM_PEAK_GBS},
+            "kernel_ms_per_launch": {k: v[0] / max(v[1], 1) for k, v in kt.items()},
+            "visited_windows_last_step": visited,
+            "detections_last_step": total_det,
+        }
+        if not args.no_cpu and world == 1:
+            line["cpu_baseline"] = cpu_baseline(host_frames, args.model, args.levels, args.cpu_seconds)
+            line["vs_cpu"] = value / world / line["cpu_baseline"]["value"]
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

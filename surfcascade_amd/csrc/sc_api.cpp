@@ -283,6 +283,13 @@ void check_params(const sc_scan_params &p) {
 }
 
 sc_detector *make_detector(const sc::Cascade &c, const sc_scan_params *p, int device) {
+    // host-side validation first: a bad model / parameter set is reported as
+    // such even on a machine without a GPU
+    sc_scan_params prm;
+    if (p) prm = *p;
+    else sc_scan_params_default(&prm);
+    check_params(prm);
+    sc::validate_for_detect(c, (int)sc::extract_patches(prm.tmpl_w, prm.tmpl_h).size() / 4);
     int ndev = 0;
     HIPCHK(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev)
@@ -297,9 +304,7 @@ sc_detector *make_detector(const sc::Cascade &c, const sc_scan_params *p, int de
     auto *d = new sc_detector();
     try {
         d->device = device;
-        if (p) d->prm = *p;
-        else sc_scan_params_default(&d->prm);
-        check_params(d->prm);
+        d->prm = prm;
         d->casc = c;
         HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         upload_model(d);

@@ -1,0 +1,92 @@
+"""Multi-rank path on CPU (gloo, world_size 2): frame sharding + the gather of
+detection records must reproduce the single-process result exactly."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import FACE_CFG, ROOT
+
+
+def _records_for(oracle, casc, frames, params, frame0, rng):
+    """Per-rank device-style record buffer (unsorted, like the GPU's atomics)."""
+    from surfcascade_amd import RECORD_DTYPE
+    recs = []
+    for f in range(len(frames)):
+        T = oracle.integral(frames[f])
+        d, _ = oracle.detect(T, casc, params, nthreads=1)
+        for r in d:
+            recs.append((f, r["level"], r["x"], r["y"], r["w"], r["h"], r["stage"], 0, r["score"]))
+    a = np.array(recs, RECORD_DTYPE)
+    rng.shuffle(a)
+    return a
+
+
+def _worker(rank, world, port, n_frames, out_q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as O
+    from surfcascade_amd import RECORD_DTYPE, synth
+    from surfcascade_amd.dist import gather_detections, merge_records, shard_range
+    casc = O.cascade_from_cfg(open(FACE_CFG).read())
+    casc.theta[:] = np.float32(0.45)  # permissive: plenty of detections
+    params = O.Params(n_levels=2)
+    start, cnt = shard_range(n_frames, world, rank)
+    frames = np.stack([synth.make_frame(320, 240, 500 + start + k) for k in range(cnt)])
+    a = _records_for(O, casc, frames, params, start, np.random.default_rng(rank))
+    cap = 1 << 15
+    buf = np.zeros(cap, RECORD_DTYPE)
+    buf[:len(a)] = a
+    B = max(shard_range(n_frames, world, r)[1] for r in range(world))
+    counts = np.zeros(1 + B, np.int32)
+    counts[0] = len(a)
+    for f in range(cnt):
+        counts[1 + f] = int((a["frame"] == f).sum())
+    gc, gr = gather_detections(torch.from_numpy(counts), torch.from_numpy(buf.view(np.uint8).copy()))
+    offs = [shard_range(n_frames, world, r)[0] for r in range(world)]
+    merged = merge_records(gc, gr, offs)
+    if rank == 0:
+        out_q.put(merged.tobytes())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_range_covers_all():
+    from surfcascade_amd.dist import shard_range
+    for n, w in ((256, 8), (10, 3), (3, 4)):
+        seen = []
+        for r in range(w):
+            s, c = shard_range(n, w, r)
+            seen += list(range(s, s + c))
+        assert seen == list(range(n))
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_gather_equals_single_process(oracle, world):
+    from surfcascade_amd import RECORD_DTYPE, synth
+    from surfcascade_amd.dist import merge_records
+    n_frames = 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_frames, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = np.frombuffer(q.get(timeout=120), RECORD_DTYPE)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # single process reference
+    casc = oracle.cascade_from_cfg(open(FACE_CFG).read())
+    casc.theta[:] = np.float32(0.45)
+    params = oracle.Params(n_levels=2)
+    frames = np.stack([synth.make_frame(320, 240, 500 + k) for k in range(n_frames)])
+    a = _records_for(oracle, casc, frames, params, 0, np.random.default_rng(9))
+    ref = merge_records([np.array([len(a)])], [a.view(np.uint8)], [0])
+    assert len(ref) > 50
+    assert got.tobytes() == ref.tobytes()
