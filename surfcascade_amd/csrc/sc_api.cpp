@@ -63,7 +63,8 @@ struct DevBuf {
 
 struct Geometry {
     int W = 0, H = 0;
-    int n_levels = 0, step = 1, pitch_cells = 0, nx_max = 0;
+    int n_levels = 0, step = 1, nx_max = 0;
+    sc::TableGeom tg{};
     long long grid = 0;
     std::vector<sc::LevelInfo> levels;
     std::vector<int2> rows;
@@ -91,7 +92,7 @@ struct sc_detector {
     DevBuf<sc::ProjPatch> d_proj;
     // working buffers
     DevBuf<uint8_t> d_frames;
-    DevBuf<float> d_table;
+    DevBuf<float4> d_table;
     int table_frames = 0;
     DevBuf<sc_det_record> d_out;
     DevBuf<int> d_counters;
@@ -168,7 +169,20 @@ void build_geometry(sc_detector *d, int W, int H) {
     ng.step = ref_step(p);
     ng.n_levels = ref_levels(W, H, p);
     if (ng.n_levels < 0 || ng.n_levels > 256) throw Error{SC_ERR_INVALID, "bad level count"};
-    ng.pitch_cells = ((W + 1) + 3) & ~3;
+    {   // phase-split table geometry (sc_kernels.hpp)
+        sc::TableGeom &t = ng.tg;
+        t.W = W;
+        t.H = H;
+        t.step = ng.step;
+        const int Q = (W + 1 + ng.step - 1) / ng.step;
+        t.Qp = (Q + 15) & ~15;
+        t.rowp = 2 * ng.step * t.Qp;
+        t.frame4 = (long long)(H + 1) * t.rowp;
+        if ((long long)(H + 1) * t.rowp > (1ll << 30))
+            throw Error{SC_ERR_INVALID, "frame too large for 32-bit table offsets"};
+    }
+    const sc::TableGeom &tg = ng.tg;
+    auto col_off = [&](int cx) { return (cx % tg.step) * tg.Qp + cx / tg.step; };
     ng.proj.resize((size_t)ng.n_levels * d->K);
     long long gb = 0;
     for (int i = 0; i < ng.n_levels; i++) {
@@ -180,6 +194,8 @@ void build_geometry(sc_detector *d, int W, int H) {
         if (L.l >= 1 && L.l <= W && L.lh <= H) {
             L.nx = (W - L.l) / ng.step + 1;
             L.ny = (H - L.lh) / ng.step + 1;
+            L.pre_col = col_off(L.l);
+            L.pre_row = L.lh * tg.rowp;
             if (L.nx > 65535) throw Error{SC_ERR_INVALID, "too many windows per row"};
             for (int r = 0; r < L.ny; r++) ng.rows.push_back(make_int2(i, r * ng.step));
             gb += (long long)L.nx * L.ny;
@@ -201,25 +217,25 @@ void build_geometry(sc_detector *d, int W, int H) {
                 ph = pw * ratio;
             }
             sc::ProjPatch pp{};
-            int gw, gh;
+            int gw, gh, c;
             if (pw == ph) {
-                pp.c = (int16_t)(pw / 2);
+                c = pw / 2;
                 pp.shape = 0;
                 gw = gh = 2;
             } else {
-                int c = std::min(pw, ph);
-                pp.c = (int16_t)c;
+                c = std::min(pw, ph);
                 pp.shape = pw < ph ? 1 : 2;
                 gw = pw / std::max(c, 1);
                 gh = ph / std::max(c, 1);
             }
-            if (pp.c <= 0)
+            if (c <= 0)
                 throw Error{SC_ERR_INVALID, "projected cell edge is 0 at level " + std::to_string(i)};
-            pp.dx = (int16_t)px;
-            pp.dy = (int16_t)py;
-            if (L.nx > 0 && (px + gw * pp.c > L.l || py + gh * pp.c > L.lh))
+            if (L.nx > 0 && (px + gw * c > L.l || py + gh * c > L.lh))
                 throw Error{SC_ERR_INVALID, "projected patch leaves the window at level " +
                                                 std::to_string(i)};
+            pp.row0 = py * tg.rowp;
+            pp.rowstep = c * tg.rowp;
+            for (int q = 0; q <= gw; q++) pp.col[q] = col_off(px + q * c);
             ng.proj[(size_t)i * d->K + k] = pp;
         }
         ng.levels.push_back(L);
@@ -317,8 +333,7 @@ sc_detector *make_detector(const sc::Cascade &c, const sc_scan_params *p, int de
 
 void ensure_buffers(sc_detector *d, int n) {
     const Geometry &g = d->geo;
-    const size_t frame_floats = (size_t)(g.H + 1) * g.pitch_cells * 8;
-    d->d_table.ensure(frame_floats * n);
+    d->d_table.ensure((size_t)g.tg.frame4 * n);
     d->d_counters.ensure((size_t)n + 1);
     d->d_visited.ensure(1);
     if (d->debug) {
@@ -346,12 +361,10 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     build_geometry(d, W, H);
     ensure_buffers(d, n);
     const Geometry &g = d->geo;
-    const long long frame_floats = (long long)(g.H + 1) * g.pitch_cells * 8;
-    const int pitch = g.pitch_cells * 8;
     HIPCHK(hipMemsetAsync(d_counts, 0, sizeof(int) * (n + 1), d->stream));
     HIPCHK(hipMemsetAsync(d->d_visited.p, 0, sizeof(unsigned long long), d->stream));
 
-    sc::RowScanArgs ra{d_frames, (long long)H * stride, stride, W, H, d->d_table.p, frame_floats, pitch};
+    sc::RowScanArgs ra{d_frames, (long long)H * stride, stride, d->d_table.p, g.tg};
     hipEvent_t e0 = nullptr;
     timed_begin(d, &e0);
     sc::launch_rowscan(ra, n, d->stream);
@@ -359,14 +372,13 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     timed_end(d, SC_KERNEL_ROWSCAN, e0);
 
     timed_begin(d, &e0);
-    sc::launch_colscan(d->d_table.p, frame_floats, pitch, W, H, n, d->stream);
+    sc::launch_colscan(d->d_table.p, g.tg, n, d->stream);
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_COLSCAN, e0);
 
     sc::WindowArgs wa{};
     wa.table = d->d_table.p;
-    wa.frame_stride = frame_floats;
-    wa.pitch = pitch;
+    wa.g = g.tg;
     wa.rows = d->d_rows.p;
     wa.levels = d->d_levels.p;
     wa.proj = d->d_proj.p;
@@ -376,7 +388,6 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     wa.stage_off = d->d_stage_off.p;
     wa.K = d->K;
     wa.n_stages = d->S;
-    wa.step = g.step;
     wa.stride_score = d->prm.stride_score;
     wa.out = d_out;
     wa.capacity = capacity;
@@ -629,7 +640,7 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value) {
         case SC_INFO_LEVELS: *value = d->geo.n_levels; break;
         case SC_INFO_GRID_WINDOWS: *value = d->geo.grid; break;
         case SC_INFO_ROWS: *value = (int64_t)d->geo.rows.size(); break;
-        case SC_INFO_TABLE_PITCH: *value = d->geo.pitch_cells; break;
+        case SC_INFO_TABLE_PITCH: *value = d->geo.tg.rowp; break;
         case SC_INFO_VISITED: *value = d->last_visited; break;
         default: return fail(SC_ERR_INVALID, "unknown info key");
     }
@@ -650,11 +661,23 @@ int sc_debug_dump(sc_detector *d, int what, int frame, void *dst, size_t bytes) 
         HIPCHK(hipStreamSynchronize(d->stream));
         const Geometry &g = d->geo;
         if (what == SC_DUMP_INTEGRAL) {
-            const size_t row = (size_t)(g.W + 1) * 32, need = row * (g.H + 1);
+            // back to the reference's interleaved S[y][x][8] layout
+            const size_t need = (size_t)(g.W + 1) * 32 * (g.H + 1);
             if (bytes < need) throw Error{SC_ERR_CAPACITY, "dump buffer too small"};
-            const float *src = d->d_table.p + (size_t)frame * (g.H + 1) * g.pitch_cells * 8;
-            HIPCHK(hipMemcpy2D(dst, row, src, (size_t)g.pitch_cells * 32, row, g.H + 1,
-                               hipMemcpyDeviceToHost));
+            const sc::TableGeom &t = g.tg;
+            std::vector<float4> tab((size_t)t.frame4);
+            HIPCHK(hipMemcpy(tab.data(), d->d_table.p + (size_t)frame * t.frame4,
+                             tab.size() * sizeof(float4), hipMemcpyDeviceToHost));
+            float *o = static_cast<float *>(dst);
+            for (int y = 0; y <= g.H; y++)
+                for (int x = 0; x <= g.W; x++) {
+                    const size_t base = (size_t)y * t.rowp + x / t.step;
+                    const float4 lo = tab[base + (size_t)(x % t.step) * t.Qp];
+                    const float4 hi = tab[base + (size_t)(t.step + x % t.step) * t.Qp];
+                    float *c = o + ((size_t)y * (g.W + 1) + x) * 8;
+                    c[0] = lo.x; c[1] = lo.y; c[2] = lo.z; c[3] = lo.w;
+                    c[4] = hi.x; c[5] = hi.y; c[6] = hi.z; c[7] = hi.w;
+                }
             return SC_OK;
         }
         if (!d->debug) throw Error{SC_ERR_INVALID, "debug records disabled (sc_detector_set_debug)"};

@@ -2,24 +2,24 @@
 //
 //   rowscan  : T2bFilter gradients (DenseSURFFeatureExtractor.cpp:199-349)
 //              fused with the exact integer row prefix of cv::integral
-//              (:73-76); writes R_y[x] (exact in f32) into the table rows.
+//              (:73-76); writes R_y[x] (exact in f32) into table row y+1.
 //   colscan  : the f32 column recurrence S[y+1][x] = S[y][x] + R_y[x],
 //              sequential in y per (x, channel) -- the association order of
-//              OpenCV's scalar integral_; table layout = F256Dat interleave
-//              (.h:21-25, merge :80).
+//              OpenCV's scalar integral_.
 //   windows  : one workgroup per (frame, level, row y): prefilter
 //              (sum(), :351-358 / ObjDetector.cpp:188), then the cascade
 //              stage by stage over a compacted survivor list (ballot +
-//              prefix), (window, weak) items spread over all lanes; each item
+//              prefix), (window, weak) items spread over all lanes k-major so
+//              a wave gathers the same corner of consecutive windows; each item
 //              is ProjectPatches/CalcFeature/Normalize/LogisticRegression::
 //              Predict (:459-484, :379-457, LogisticRegression.cpp:46-68);
 //              stage sums in weak order (GentleAdaboost.cpp:247-261); finally
-//              the adaptive-stride x walk of ObjDetector.cpp:185-217 over
-//              the row's results, emitting detections.
+//              the adaptive-stride x walk of ObjDetector.cpp:185-217 over the
+//              row's results, emitting detections.
 //
 // Every f32/f64 operation is the one the reference performs, in its order;
 // the file is compiled with -ffp-contract=off (no FMA contraction), IEEE
-// sqrt / division (hipcc default), no fast-math.
+// sqrt / division (hipcc default), no fast-math.  Table layout: sc_kernels.hpp.
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -32,39 +32,46 @@ namespace sc {
 namespace {
 
 constexpr int kRowThreads = 256;
-constexpr int kRowSeg = kRowThreads * 8;  // pixels per rowscan segment
+constexpr int kRowPx = 4;                      // pixels per thread
+constexpr int kRowSeg = kRowThreads * kRowPx;  // pixels per segment
 constexpr int kWinThreads = 256;
 constexpr int kWaves = kWinThreads / 64;
 
 __device__ __forceinline__ uint32_t sat_sub(uint32_t a, uint32_t b) { return a > b ? a - b : 0u; }
 
 // ---------------------------------------------------------------------------
-// rowscan: gradients + exact integer row prefix -> table rows 1..H
+// rowscan: gradients + exact integer row prefix -> table row y+1
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kRowThreads) void rowscan_kernel(RowScanArgs a) {
     __shared__ uint8_t s_img[3][kRowSeg + 16];
+    __shared__ __attribute__((aligned(16))) float s_out[kRowSeg * 8];
     __shared__ uint32_t s_wsum[kRowThreads / 64][8];
 
     const int y = blockIdx.x, frame = blockIdx.y, tid = threadIdx.x;
     const int lane = tid & 63, wv = tid >> 6;
-    const int W = a.W, H = a.H;
+    const TableGeom g = a.g;
+    const int W = g.W, H = g.H, step = g.step, Qp = g.Qp;
     const uint8_t *img = a.frames + (long long)frame * a.frame_bytes;
     const uint8_t *rows[3] = {img + (long long)(y > 0 ? y - 1 : 0) * a.stride,
                               img + (long long)y * a.stride,
                               img + (long long)(y < H - 1 ? y + 1 : H - 1) * a.stride};
-    float *tab = a.table + (long long)frame * a.frame_stride;
-    float *out = tab + (long long)(y + 1) * a.pitch;
+    float4 *tab = a.table + (long long)frame * g.frame4;
+    float4 *out = tab + (long long)(y + 1) * g.rowp;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
 
     if (y == 0)  // table row 0 is all zeros
-        for (int i = tid; i < a.pitch; i += kRowThreads) tab[i] = 0.0f;
-    if (tid < 8) out[tid] = 0.0f;  // column 0
+        for (int i = tid; i < g.rowp; i += kRowThreads) tab[i] = z4;
+    if (tid == 0) {  // column 0 (phase 0, q 0) of this row
+        out[0] = z4;
+        out[(long long)step * Qp] = z4;
+    }
 
     uint32_t carry[8];
 #pragma unroll
     for (int c = 0; c < 8; c++) carry[c] = 0;
 
     for (int seg = 0; seg < W; seg += kRowSeg) {
-        // stage the three source rows of this segment (x = seg-1 .. seg+2048)
+        // stage the three source rows of this segment (x = seg-1 .. seg+kRowSeg)
         for (int i = tid; i < kRowSeg + 2; i += kRowThreads) {
             int x = seg - 1 + i;
             x = x < 0 ? 0 : (x > W - 1 ? W - 1 : x);
@@ -73,13 +80,13 @@ __global__ __launch_bounds__(kRowThreads) void rowscan_kernel(RowScanArgs a) {
         }
         __syncthreads();
 
-        const int x0 = seg + tid * 8;
-        uint32_t pre[8][8];  // inclusive in-thread prefix [px][ch]
+        const int x0 = seg + tid * kRowPx;
+        uint32_t pre[kRowPx][8];  // inclusive in-thread prefix [px][ch]
         uint32_t acc[8];
 #pragma unroll
         for (int c = 0; c < 8; c++) acc[c] = 0;
 #pragma unroll
-        for (int px = 0; px < 8; px++) {
+        for (int px = 0; px < kRowPx; px++) {
             const int x = x0 + px;
             if (x < W) {
                 const int xn = (x < W - 1 ? x + 1 : W - 1) - seg + 1;
@@ -121,6 +128,7 @@ __global__ __launch_bounds__(kRowThreads) void rowscan_kernel(RowScanArgs a) {
 #pragma unroll
         for (int c = 0; c < 8; c++) {
             uint32_t b = 0, t = 0;
+#pragma unroll
             for (int w = 0; w < kRowThreads / 64; w++) {
                 if (w < wv) b += s_wsum[w][c];
                 t += s_wsum[w][c];
@@ -128,22 +136,31 @@ __global__ __launch_bounds__(kRowThreads) void rowscan_kernel(RowScanArgs a) {
             base[c] = carry[c] + b + incl[c] - acc[c];
             seg_total[c] = t;
         }
+        // R values (exact integers < 2^24, exact in f32) staged in LDS
 #pragma unroll
-        for (int px = 0; px < 8; px++) {
-            const int x = x0 + px;
-            if (x < W) {
-                float4 lo, hi;
-                lo.x = (float)(base[0] + pre[px][0]);
-                lo.y = (float)(base[1] + pre[px][1]);
-                lo.z = (float)(base[2] + pre[px][2]);
-                lo.w = (float)(base[3] + pre[px][3]);
-                hi.x = (float)(base[4] + pre[px][4]);
-                hi.y = (float)(base[5] + pre[px][5]);
-                hi.z = (float)(base[6] + pre[px][6]);
-                hi.w = (float)(base[7] + pre[px][7]);
-                float4 *dst = reinterpret_cast<float4 *>(out + (long long)(x + 1) * 8);
-                dst[0] = lo;
-                dst[1] = hi;
+        for (int px = 0; px < kRowPx; px++) {
+            float4 lo, hi;
+            lo.x = (float)(base[0] + pre[px][0]);
+            lo.y = (float)(base[1] + pre[px][1]);
+            lo.z = (float)(base[2] + pre[px][2]);
+            lo.w = (float)(base[3] + pre[px][3]);
+            hi.x = (float)(base[4] + pre[px][4]);
+            hi.y = (float)(base[5] + pre[px][5]);
+            hi.z = (float)(base[6] + pre[px][6]);
+            hi.w = (float)(base[7] + pre[px][7]);
+            float4 *d = reinterpret_cast<float4 *>(s_out + (tid * kRowPx + px) * 8);
+            d[0] = lo;
+            d[1] = hi;
+        }
+        __syncthreads();
+        // phase-split stores: cell X = seg+1+i -> (X % step, X / step)
+        for (int i = tid; i < kRowSeg; i += kRowThreads) {
+            const int X = seg + 1 + i;
+            if (X <= W) {
+                const int q = X / step, p = X - q * step;
+                const float4 *src = reinterpret_cast<const float4 *>(s_out + i * 8);
+                out[(long long)p * Qp + q] = src[0];
+                out[(long long)(step + p) * Qp + q] = src[1];
             }
         }
 #pragma unroll
@@ -157,25 +174,30 @@ __global__ __launch_bounds__(kRowThreads) void rowscan_kernel(RowScanArgs a) {
 // ---------------------------------------------------------------------------
 constexpr int kColBlk = 32;
 
-__global__ __launch_bounds__(64) void colscan_kernel(float *table, long long frame_stride,
-                                                     int pitch, int W, int H) {
-    const int idx = blockIdx.x * 64 + threadIdx.x;
-    if (idx >= (W + 1) * 8) return;
-    float *col = table + (long long)blockIdx.y * frame_stride + idx;
+__global__ __launch_bounds__(64) void colscan_kernel(float *table, TableGeom g) {
+    const int fi = blockIdx.x * 64 + threadIdx.x;  // float index within a row
+    if (fi >= g.rowp * 4) return;
+    {   // skip padding cells (x > W) -- never written, never read
+        const int f4 = fi >> 2, plane = f4 / g.Qp, q = f4 - plane * g.Qp;
+        const int p = plane % g.step;
+        if (q * g.step + p > g.W) return;
+    }
+    const long long pitch = (long long)g.rowp * 4;
+    const int H = g.H;
+    float *col = table + (long long)blockIdx.y * g.frame4 * 4 + fi;
     float acc = 0.0f;  // row 0
     float cur[kColBlk], nxt[kColBlk];
 #pragma unroll
-    for (int k = 0; k < kColBlk; k++) cur[k] = (1 + k <= H) ? col[(long long)(1 + k) * pitch] : 0.0f;
+    for (int k = 0; k < kColBlk; k++) cur[k] = (1 + k <= H) ? col[(1 + k) * pitch] : 0.0f;
     for (int y = 1; y <= H; y += kColBlk) {
         const int yn = y + kColBlk;
 #pragma unroll
-        for (int k = 0; k < kColBlk; k++)
-            nxt[k] = (yn + k <= H) ? col[(long long)(yn + k) * pitch] : 0.0f;
+        for (int k = 0; k < kColBlk; k++) nxt[k] = (yn + k <= H) ? col[(yn + k) * pitch] : 0.0f;
 #pragma unroll
         for (int k = 0; k < kColBlk; k++) {
             if (y + k <= H) {
                 acc = acc + cur[k];
-                col[(long long)(y + k) * pitch] = acc;
+                col[(y + k) * pitch] = acc;
             }
         }
 #pragma unroll
@@ -187,8 +209,6 @@ __global__ __launch_bounds__(64) void colscan_kernel(float *table, long long fra
 // windows
 // ---------------------------------------------------------------------------
 
-__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
-
 // (TL + BR) - (TR + BL) per lane (DenseSURFFeatureExtractor.cpp:385-412).
 __device__ __forceinline__ float4 box4(float4 tl, float4 br, float4 tr, float4 bl) {
     float4 r;
@@ -197,15 +217,6 @@ __device__ __forceinline__ float4 box4(float4 tl, float4 br, float4 tr, float4 b
     r.z = (tl.z + br.z) - (tr.z + bl.z);
     r.w = (tl.w + br.w) - (tr.w + bl.w);
     return r;
-}
-
-// sum(win) > area*k  (DenseSURFFeatureExtractor.cpp:351-358, ObjDetector.cpp:188)
-__device__ __forceinline__ bool prefilter(const float *T, int pitch, int x, int y, int w, int h,
-                                          float thr) {
-    const float *r0 = T + (long long)y * pitch, *r1 = T + (long long)(y + h) * pitch;
-    float4 v = box4(ld4(r0 + x * 8), ld4(r1 + (x + w) * 8), ld4(r0 + (x + w) * 8), ld4(r1 + x * 8));
-    float m = (((v.x + v.y) + v.z) + v.w) / 2.0f;
-    return m > thr;
 }
 
 // c_k = (q0+q1)+(q2+q3); SS = (((eps + c0) + c1) ...) + c7   (:427-433)
@@ -220,24 +231,45 @@ __device__ __forceinline__ float ss_hadd(const float (&f)[32]) {
     return ss;
 }
 
-// One (window, weak classifier) item: CalcFeature + Normalize + Predict.
-__device__ float weak_eval(const float *T, int pitch, int X, int Y, ProjPatch pj,
-                           const float4 *__restrict__ w4, double bias) {
-    const int x0 = X + pj.dx, y0 = Y + pj.dy, c = pj.c;
-    const int gw = pj.shape == 1 ? 1 : (pj.shape == 2 ? 4 : 2);
-    float f[32];
+// The 32 box sums of one projected patch: corners deduplicated on the
+// (GW+1) x (GH+1) corner grid; cell index = row*GW + col (GetRectsFromPatch).
+template <int GW, int GH>
+__device__ __forceinline__ void patch_features(const float4 *__restrict__ T, const ProjPatch &pj,
+                                               int half_off, float (&f)[32]) {
 #pragma unroll
-    for (int cell = 0; cell < 4; cell++) {
-        const int cx = cell % gw, cy = cell / gw;
-        const int xa = x0 + cx * c, ya = y0 + cy * c;
-        const float *ra = T + (long long)ya * pitch, *rb = T + (long long)(ya + c) * pitch;
-        const float *tl = ra + xa * 8, *tr = ra + (xa + c) * 8;
-        const float *bl = rb + xa * 8, *br = rb + (xa + c) * 8;
-        float4 lo = box4(ld4(tl), ld4(br), ld4(tr), ld4(bl));
-        float4 hi = box4(ld4(tl + 4), ld4(br + 4), ld4(tr + 4), ld4(bl + 4));
-        f[8 * cell + 0] = lo.x; f[8 * cell + 1] = lo.y; f[8 * cell + 2] = lo.z; f[8 * cell + 3] = lo.w;
-        f[8 * cell + 4] = hi.x; f[8 * cell + 5] = hi.y; f[8 * cell + 6] = hi.z; f[8 * cell + 7] = hi.w;
+    for (int h = 0; h < 2; h++) {
+        const float4 *Th = T + h * half_off;
+        float4 prev[GW + 1], cur[GW + 1];
+#pragma unroll
+        for (int c = 0; c <= GW; c++) prev[c] = Th[pj.row0 + pj.col[c]];
+#pragma unroll
+        for (int r = 0; r < GH; r++) {
+            const int ro = pj.row0 + (r + 1) * pj.rowstep;
+#pragma unroll
+            for (int c = 0; c <= GW; c++) cur[c] = Th[ro + pj.col[c]];
+#pragma unroll
+            for (int c = 0; c < GW; c++) {
+                const float4 v = box4(prev[c], cur[c + 1], prev[c + 1], cur[c]);
+                const int o = 8 * (r * GW + c) + 4 * h;
+                f[o + 0] = v.x;
+                f[o + 1] = v.y;
+                f[o + 2] = v.z;
+                f[o + 3] = v.w;
+            }
+#pragma unroll
+            for (int c = 0; c <= GW; c++) prev[c] = cur[c];
+        }
     }
+}
+
+// One (window, weak classifier) item: CalcFeature + Normalize + Predict.
+// T points at the window's origin cell (row y, window j) in half 0.
+__device__ float weak_eval(const float4 *__restrict__ T, int half_off, const ProjPatch &pj,
+                           const float4 *__restrict__ w4, double bias) {
+    float f[32];
+    if (pj.shape == 0) patch_features<2, 2>(T, pj, half_off, f);
+    else if (pj.shape == 1) patch_features<1, 4>(T, pj, half_off, f);
+    else patch_features<4, 1>(T, pj, half_off, f);
     // Normalize (:417-457): clip at sqrt(SS)*theta, renormalise by 1/sqrt(SS2)
     const float theta = 0.35355338f;  // 2/sqrt(32.f) (.h:36)
     const float t = sqrtf(ss_hadd(f)) * theta, nt = -t;
@@ -270,9 +302,9 @@ struct WinSmem {
     int *cnt;  // [kWaves]
     float *st_s;
     float *sums;
+    float *P;  // [kWinThreads]
     int16_t *st_p;
     uint16_t *surv;
-    float *P;  // [kWinThreads]
 };
 
 __device__ __forceinline__ WinSmem carve(unsigned char *smem, int nxa) {
@@ -312,11 +344,11 @@ __global__ __launch_bounds__(kWinThreads) void window_kernel(WindowArgs a) {
     const int row = blockIdx.x, frame = blockIdx.y;
     const int2 rd = a.rows[row];
     const LevelInfo L = a.levels[rd.x];
-    const int y = rd.y, nx = L.nx, step = a.step;
-    const int nxa = a.lds_nx;
-    WinSmem sm = carve(smem, nxa);
-    const float *T = a.table + (long long)frame * a.frame_stride;
-    const int pitch = a.pitch;
+    const int y = rd.y, nx = L.nx;
+    const int step = a.g.step, half_off = a.g.step * a.g.Qp;
+    WinSmem sm = carve(smem, a.lds_nx);
+    // origin cell of window 0 of this row (phase 0), half 0
+    const float4 *T = a.table + (long long)frame * a.g.frame4 + (long long)y * a.g.rowp;
 
     // 1) prefilter over the whole row; survivors in x order
     int nsurv = 0;
@@ -324,7 +356,10 @@ __global__ __launch_bounds__(kWinThreads) void window_kernel(WindowArgs a) {
         const int j = b + tid;
         bool pass = false;
         if (j < nx) {
-            pass = prefilter(T, pitch, j * step, y, L.l, L.lh, L.thr);
+            const float4 *t0 = T + j;
+            const float4 v = box4(t0[0], t0[L.pre_row + L.pre_col], t0[L.pre_col], t0[L.pre_row]);
+            const float m = (((v.x + v.y) + v.z) + v.w) / 2.0f;  // sum(), :351-358
+            pass = m > L.thr;                                    // ObjDetector.cpp:188
             sm.st_p[j] = pass ? 0 : -1;
             sm.st_s[j] = 0.0f;
         }
@@ -343,14 +378,15 @@ __global__ __launch_bounds__(kWinThreads) void window_kernel(WindowArgs a) {
             if (t < items) {
                 const int k = t / nsurv, i = t - k * nsurv;
                 const int j = sm.surv[i];
-                const int g = off + k;
-                sm.P[tid] = weak_eval(T, pitch, j * step, y, projL[g], a.w + (long long)g * 9, a.bias[g]);
+                const int gk = off + k;
+                const ProjPatch pj = projL[gk];
+                sm.P[tid] = weak_eval(T + j, half_off, pj, a.w + (long long)gk * 9, a.bias[gk]);
             }
             __syncthreads();
             const int rend = min(r + kWinThreads, items);
             for (int i = tid; i < nsurv; i += kWinThreads) {
                 // items of slot i in [r, rend): t = k*nsurv + i, in increasing k
-                int k = (r > i) ? (r - i + nsurv - 1) / nsurv : 0;
+                const int k = (r > i) ? (r - i + nsurv - 1) / nsurv : 0;
                 float acc = sm.sums[i];
                 for (int t2 = k * nsurv + i; t2 < rend; t2 += nsurv) acc += sm.P[t2 - r];
                 sm.sums[i] = acc;
@@ -450,18 +486,16 @@ __global__ __launch_bounds__(kWinThreads) void window_kernel(WindowArgs a) {
 }  // namespace
 
 void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
-    hipLaunchKernelGGL(rowscan_kernel, dim3(a.H, n_frames), dim3(kRowThreads), 0, s, a);
+    hipLaunchKernelGGL(rowscan_kernel, dim3(a.g.H, n_frames), dim3(kRowThreads), 0, s, a);
 }
 
-void launch_colscan(float *table, long long frame_stride, int pitch, int W, int H, int n_frames,
-                    hipStream_t s) {
-    const int n = (W + 1) * 8;
-    hipLaunchKernelGGL(colscan_kernel, dim3((n + 63) / 64, n_frames), dim3(64), 0, s, table,
-                       frame_stride, pitch, W, H);
+void launch_colscan(float4 *table, const TableGeom &g, int n_frames, hipStream_t s) {
+    const int n = g.rowp * 4;
+    hipLaunchKernelGGL(colscan_kernel, dim3((n + 63) / 64, n_frames), dim3(64), 0, s,
+                       reinterpret_cast<float *>(table), g);
 }
 
-size_t window_lds_bytes(int nx_max) {
-    const int nxa = (nx_max + 63) & ~63;
+size_t window_lds_bytes(int nxa) {
     return 16 + (size_t)nxa * 4 * 2 + kWinThreads * 4 + (size_t)nxa * 2 * 2;
 }
 

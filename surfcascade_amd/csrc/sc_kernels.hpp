@@ -1,4 +1,14 @@
 // sc_kernels.hpp -- launch interface of the gfx950 kernels (sc_kernels.hip).
+//
+// Integral-table layout in HBM ("phase-split"): the reference's table is
+// S[y][x][8 channels] (F256Dat, DenseSURFFeatureExtractor.h:21-25).  Windows
+// of one row sit at x = step*j, so the corner a weak classifier reads for
+// window j is at x = step*j + off: always the same phase off % step.  We store
+// each table row as 2 halves (channels 0-3, 4-7) x `step` phase planes x Qp
+// float4 cells:   cell(y, x, half) = y*rowp + (half*step + x%step)*Qp + x/step
+// so lanes working on consecutive windows read consecutive float4s (1 KiB per
+// wave instruction).  Values are bit-identical to the reference table; only
+// the addressing differs (sc_debug_dump converts back).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -9,38 +19,45 @@
 
 namespace sc {
 
-// One scale level of the window pyramid (ObjDetector.cpp:178-182).
-struct LevelInfo {
-    int l, lh;          // window width / height
-    int nx, ny;         // grid windows per row / rows
-    long long grid_base;  // first grid index of the level (canonical order)
-    float thr;          // (float)(l*lh) * prefilter_k   (ObjDetector.cpp:188)
-    int pad;
+struct TableGeom {
+    int W, H, step;
+    int Qp;    // float4 cells per phase plane (>= ceil((W+1)/step), multiple of 16)
+    int rowp;  // float4 per table row = 2*step*Qp
+    long long frame4;  // float4 per frame table = (H+1)*rowp
 };
 
-// Projected template patch of one weak classifier at one level
-// (ProjectPatches + GetRectsFromPatch, DenseSURFFeatureExtractor.cpp:459-484,
-// 360-377): corner offsets relative to the window origin.
+// One scale level of the window pyramid (ObjDetector.cpp:178-182).
+struct LevelInfo {
+    int l, lh;            // window width / height
+    int nx, ny;           // grid windows per row / rows
+    long long grid_base;  // first grid index of the level (canonical order)
+    float thr;            // (float)(l*lh) * prefilter_k   (ObjDetector.cpp:188)
+    int pre_col;          // cell offset of column x+l: (l%step)*Qp + l/step
+    int pre_row;          // lh*rowp
+    int pad[3];
+};
+
+// A fitted patch projected to one level (ProjectPatches + GetRectsFromPatch,
+// DenseSURFFeatureExtractor.cpp:459-484, 360-377), as table offsets relative
+// to the window's origin cell.  shape 0: 2x2 cells, 1: 1x4 (tall), 2: 4x1.
 struct ProjPatch {
-    int16_t dx, dy;  // projected patch origin
-    int16_t c;       // cell edge
-    int16_t shape;   // 0: 2x2, 1: 1x4 (tall), 2: 4x1 (wide)
+    int shape;
+    int row0;     // dy*rowp
+    int rowstep;  // c*rowp
+    int col[5];   // ((dx+i*c)%step)*Qp + (dx+i*c)/step, i = 0..gw
 };
 
 struct RowScanArgs {
     const uint8_t *frames;
     long long frame_bytes;  // distance between frames
     int stride;             // bytes per image row
-    int W, H;
-    float *table;
-    long long frame_stride;  // floats between frame tables
-    int pitch;               // floats per table row (cells*8)
+    float4 *table;
+    TableGeom g;
 };
 
 struct WindowArgs {
-    const float *table;
-    long long frame_stride;
-    int pitch;
+    const float4 *table;
+    TableGeom g;
     const int2 *rows;  // (level, y)
     const LevelInfo *levels;
     const ProjPatch *proj;  // [n_levels][K]
@@ -48,23 +65,22 @@ struct WindowArgs {
     const double *bias;     // [K]
     const float *theta;     // [S]
     const int *stage_off;   // [S+1]
-    int K, n_stages, step;
+    int K, n_stages;
     double stride_score;
     sc_det_record *out;
     int capacity;
     int *counters;  // [0] total, [1+f] per frame
     unsigned long long *visited;
-    // debug (grid-indexed per frame) -- only written when non-null
+    // debug (grid-indexed per frame) -- only written by the debug variant
     int16_t *dbg_p;
     float *dbg_s;
     uint8_t *dbg_v;
     long long grid_per_frame;
-    int lds_nx;  // windows per row the dynamic LDS is sized for
+    int lds_nx;  // windows per row the dynamic LDS is sized for (multiple of 64)
 };
 
 void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s);
-void launch_colscan(float *table, long long frame_stride, int pitch, int W, int H,
-                    int n_frames, hipStream_t s);
+void launch_colscan(float4 *table, const TableGeom &g, int n_frames, hipStream_t s);
 void launch_windows(const WindowArgs &a, int n_rows, int n_frames, bool debug, hipStream_t s);
 size_t window_lds_bytes(int nx_max);
 
