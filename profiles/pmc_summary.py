@@ -1,0 +1,58 @@
+"""Summarise rocprofv3 --pmc passes (profiles/collect_pmc.sh) per kernel.
+
+HBM bytes per launch follow MI355X_MICROARCH.md's HBM section: FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
+coalesced streaming read, so it is doubled (uncalibrated for other access
+shapes -- see DESIGN.md).
+usage: python profiles/pmc_summary.py gpurun_out/pmc1 [--json out.json --batch 16 ...]
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+KERNELS = {"window_kernel": "windows", "rowscan_kernel": "rowscan", "colscan_kernel": "colscan"}
+
+
+def load(d):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(d, "*", "pmc_counter_collection.csv")):
+        for row in csv.DictReader(open(f)):
+            name = next((v for k, v in KERNELS.items() if k in row["Kernel_Name"]), None)
+            if name is None:
+                continue
+            acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--json")
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--levels", type=int, default=24)
+    a = ap.parse_args()
+    res = load(a.dir)
+    for k, cs in sorted(res.items()):
+        print(k)
+        for c, v in sorted(cs.items()):
+            print("   %-28s %.6g" % (c, v))
+        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+            hbm = (2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024
+            print("   %-28s %.6g" % ("hbm_bytes_per_launch", hbm))
+    if a.json and "windows" in res:
+        cs = res["windows"]
+        out = {"batch": a.batch, "width": a.width, "height": a.height, "levels": a.levels,
+               "source": a.dir, "counters_per_launch": cs,
+               "hbm_bytes_per_launch": (2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024,
+               "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md HBM section (gfx950 reports 1/2 "
+                       "of wide coalesced reads); KiB units"}
+        json.dump(out, open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

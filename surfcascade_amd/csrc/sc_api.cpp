@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
@@ -400,6 +401,10 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     }
     wa.grid_per_frame = g.grid;
     wa.lds_nx = (g.nx_max + 63) & ~63;
+    {   // timing ablations for profiling only (wrong results); never set in production
+        static const char *v = std::getenv("SC_VARIANT");
+        wa.variant = v ? std::atoi(v) : 0;
+    }
     d->last_frames = n;
     if (g.rows.empty()) return;
     timed_begin(d, &e0);

@@ -265,19 +265,24 @@ __device__ __forceinline__ void patch_features(const float4 *__restrict__ T, con
 // One (window, weak classifier) item: CalcFeature + Normalize + Predict.
 // T points at the window's origin cell (row y, window j) in half 0.
 __device__ float weak_eval(const float4 *__restrict__ T, int half_off, const ProjPatch &pj,
-                           const float4 *__restrict__ w4, double bias) {
+                           const float4 *__restrict__ w4, double bias, int variant) {
     float f[32];
     if (pj.shape == 0) patch_features<2, 2>(T, pj, half_off, f);
     else if (pj.shape == 1) patch_features<1, 4>(T, pj, half_off, f);
     else patch_features<4, 1>(T, pj, half_off, f);
+    if (variant & 1) {  // timing ablation only: gathers without the math
+        float sum = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 32; i++) sum += f[i];
+        return sum;
+    }
     // Normalize (:417-457): clip at sqrt(SS)*theta, renormalise by 1/sqrt(SS2)
     const float theta = 0.35355338f;  // 2/sqrt(32.f) (.h:36)
     const float t = sqrtf(ss_hadd(f)) * theta, nt = -t;
+    // _mm_max_ps(_mm_min_ps(f, t), -t) as one v_med3_f32: identical bits here
+    // because f is a finite box sum (never NaN, never -0) and t > 0 (SS >= eps)
 #pragma unroll
-    for (int i = 0; i < 32; i++) {
-        float v = f[i] < t ? f[i] : t;  // _mm_min_ps
-        f[i] = v > nt ? v : nt;         // _mm_max_ps
-    }
+    for (int i = 0; i < 32; i++) f[i] = __builtin_amdgcn_fmed3f(f[i], nt, t);
     const float r = 1.0f / sqrtf(ss_hadd(f));
 #pragma unroll
     for (int i = 0; i < 32; i++) f[i] = f[i] * r;
@@ -341,7 +346,19 @@ template <bool kDebug>
 __global__ __launch_bounds__(kWinThreads) void window_kernel(WindowArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
-    const int row = blockIdx.x, frame = blockIdx.y;
+    // XCD-aware block order: the dispatcher deals blocks round-robin over the
+    // 8 XCDs (b % 8 share one L2); give each XCD a contiguous run of
+    // (frame, row) so concurrently resident rows of one XCD are neighbours
+    // and share table lines in its L2.  Bijective for any grid size.
+    int row, frame;
+    {
+        const int n = a.n_rows * a.n_frames, b = blockIdx.x;
+        const int q = n >> 3, r = n & 7, x = b & 7, idx = b >> 3;
+        int lin = b;  // measured: dispatcher order is 7% faster than the XCD-band order
+        if (a.variant & 4) lin = x < r ? x * (q + 1) + idx : r * (q + 1) + (x - r) * q + idx;
+        frame = lin / a.n_rows;
+        row = lin - frame * a.n_rows;
+    }
     const int2 rd = a.rows[row];
     const LevelInfo L = a.levels[rd.x];
     const int y = rd.y, nx = L.nx;
@@ -373,14 +390,25 @@ __global__ __launch_bounds__(kWinThreads) void window_kernel(WindowArgs a) {
         for (int i = tid; i < nsurv; i += kWinThreads) sm.sums[i] = 0.0f;
         __syncthreads();
         const int items = nsurv * n;
+        const float rcp = 1.0f / (float)nsurv;
         for (int r = 0; r < items; r += kWinThreads) {
             const int t = r + tid;
             if (t < items) {
-                const int k = t / nsurv, i = t - k * nsurv;
+                // k = t / nsurv without an integer divide (t < 2^24: one correction)
+                int k = (int)((float)t * rcp), i = t - k * nsurv;
+                if (i < 0) { k--; i += nsurv; }
+                else if (i >= nsurv) { k++; i -= nsurv; }
                 const int j = sm.surv[i];
                 const int gk = off + k;
                 const ProjPatch pj = projL[gk];
-                sm.P[tid] = weak_eval(T + j, half_off, pj, a.w + (long long)gk * 9, a.bias[gk]);
+                if (a.variant & 2) {  // timing ablation only: L1-resident gathers
+                    ProjPatch z{};
+                    z.shape = pj.shape;
+                    sm.P[tid] = weak_eval(T, half_off, z, a.w + (long long)gk * 9, a.bias[gk], a.variant);
+                } else {
+                    sm.P[tid] = weak_eval(T + j, half_off, pj, a.w + (long long)gk * 9, a.bias[gk],
+                                          a.variant);
+                }
             }
             __syncthreads();
             const int rend = min(r + kWinThreads, items);
@@ -501,10 +529,14 @@ size_t window_lds_bytes(int nxa) {
 
 void launch_windows(const WindowArgs &a, int n_rows, int n_frames, bool debug, hipStream_t s) {
     const size_t lds = window_lds_bytes(a.lds_nx);
+    WindowArgs b = a;
+    b.n_rows = n_rows;
+    b.n_frames = n_frames;
+    const dim3 grid(n_rows * n_frames);
     if (debug)
-        hipLaunchKernelGGL(window_kernel<true>, dim3(n_rows, n_frames), dim3(kWinThreads), lds, s, a);
+        hipLaunchKernelGGL(window_kernel<true>, grid, dim3(kWinThreads), lds, s, b);
     else
-        hipLaunchKernelGGL(window_kernel<false>, dim3(n_rows, n_frames), dim3(kWinThreads), lds, s, a);
+        hipLaunchKernelGGL(window_kernel<false>, grid, dim3(kWinThreads), lds, s, b);
 }
 
 }  // namespace sc

@@ -77,6 +77,8 @@ struct WindowArgs {
     uint8_t *dbg_v;
     long long grid_per_frame;
     int lds_nx;  // windows per row the dynamic LDS is sized for (multiple of 64)
+    int n_rows, n_frames;  // set by launch_windows
+    int variant;           // 0 in production; timing ablations (SC_VARIANT env)
 };
 
 void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s);
