@@ -137,8 +137,9 @@ int sc_debug_dump(sc_detector *d, int what, int frame, void *dst,
 /* Per-kernel HIP-event timing on the detector's stream (bench / profiling). */
 #define SC_KERNEL_ROWSCAN 0
 #define SC_KERNEL_COLSCAN 1
-#define SC_KERNEL_WINDOWS 2
-#define SC_KERNEL_COUNT 3
+#define SC_KERNEL_WINDOWS 2 /* prefilter + cascade */
+#define SC_KERNEL_WALK 3    /* adaptive-stride walk + detections */
+#define SC_KERNEL_COUNT 4
 int sc_set_timing(sc_detector *d, int on);
 int sc_get_timing(sc_detector *d, double ms_total[SC_KERNEL_COUNT],
                   int64_t launches[SC_KERNEL_COUNT]);

@@ -35,7 +35,7 @@ RECORD_DTYPE = np.dtype([("frame", "<i4"), ("level", "<i4"), ("x", "<i4"), ("y",
                          ("w", "<i4"), ("h", "<i4"), ("stage", "<i4"), ("pad", "<i4"),
                          ("score", "<f8")])
 
-KERNELS = ("rowscan", "colscan", "windows")
+KERNELS = ("rowscan", "colscan", "windows", "walk")
 
 # every symbol include/surfcascade.h declares
 EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_model_save",
@@ -354,7 +354,7 @@ class Detector:
         _check(load_library().sc_set_timing(self._h, int(on)))
 
     def get_timing(self):
-        ms = (ctypes.c_double * 3)()
-        n = (ctypes.c_int64 * 3)()
+        ms = (ctypes.c_double * len(KERNELS))()
+        n = (ctypes.c_int64 * len(KERNELS))()
         _check(load_library().sc_get_timing(self._h, ms, n))
         return {k: (ms[i], n[i]) for i, k in enumerate(KERNELS)}

@@ -65,6 +65,7 @@ struct DevBuf {
 struct Geometry {
     int W = 0, H = 0;
     int n_levels = 0, step = 1, nx_max = 0;
+    int n_sub = 1, strip_max = 1;  // cascade tasks: 8*n_sub strips per row
     sc::TableGeom tg{};
     long long grid = 0;
     std::vector<sc::LevelInfo> levels;
@@ -97,14 +98,14 @@ struct sc_detector {
     int table_frames = 0;
     DevBuf<sc_det_record> d_out;
     DevBuf<int> d_counters;
-    DevBuf<unsigned long long> d_visited;
+    DevBuf<unsigned> d_visited;  // per (frame, row): windows the x chain visited
+    DevBuf<int> d_queues;       // per-XCD task counters of the cascade kernel
+    DevBuf<int8_t> d_st_p;      // per grid window: stage reached (-1 prefilter reject)
+    DevBuf<float> d_st_s;       // per grid window: last stage score
     // debug
     bool debug = false;
-    DevBuf<int16_t> d_dbg_p;
-    DevBuf<float> d_dbg_s;
-    DevBuf<uint8_t> d_dbg_v;
+    DevBuf<uint8_t> d_dbg_v;    // per grid window: visited by the x chain
     int last_frames = 0;
-    long long last_visited = 0;
     // timing
     bool timing = false;
     struct Pending {
@@ -113,8 +114,8 @@ struct sc_detector {
     };
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
-    double t_ms[SC_KERNEL_COUNT] = {0, 0, 0};
-    long long t_n[SC_KERNEL_COUNT] = {0, 0, 0};
+    double t_ms[SC_KERNEL_COUNT] = {};
+    long long t_n[SC_KERNEL_COUNT] = {};
 
     ~sc_detector() {
         (void)hipSetDevice(device);
@@ -127,7 +128,8 @@ struct sc_detector {
         d_w.release(); d_bias.release(); d_theta.release(); d_stage_off.release();
         d_levels.release(); d_rows.release(); d_proj.release();
         d_frames.release(); d_table.release(); d_out.release(); d_counters.release();
-        d_visited.release(); d_dbg_p.release(); d_dbg_s.release(); d_dbg_v.release();
+        d_visited.release(); d_queues.release(); d_st_p.release(); d_st_s.release();
+        d_dbg_v.release();
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -197,7 +199,8 @@ void build_geometry(sc_detector *d, int W, int H) {
             L.ny = (H - L.lh) / ng.step + 1;
             L.pre_col = col_off(L.l);
             L.pre_row = L.lh * tg.rowp;
-            if (L.nx > 65535) throw Error{SC_ERR_INVALID, "too many windows per row"};
+            if (L.nx > 4096)  // walk kernel: one wave, 64 chunks of 64 windows per row
+                throw Error{SC_ERR_INVALID, "more than 4096 windows per row (frame too wide)"};
             for (int r = 0; r < L.ny; r++) ng.rows.push_back(make_int2(i, r * ng.step));
             gb += (long long)L.nx * L.ny;
             ng.nx_max = std::max(ng.nx_max, L.nx);
@@ -242,6 +245,18 @@ void build_geometry(sc_detector *d, int W, int H) {
         ng.levels.push_back(L);
     }
     ng.grid = gb;  // may be 0: no window fits (the reference loop runs 0 times)
+    {   // cascade task size: ~72 windows per strip at the widest level
+        const char *e = std::getenv("SC_SUBSTRIPS");  // tuning override
+        ng.n_sub = e ? std::max(1, std::atoi(e))
+                     : std::max(1, (ng.nx_max + sc::kXcds * 72 / 2) / (sc::kXcds * 72));
+        const int nseg = sc::kXcds * ng.n_sub;
+        ng.strip_max = std::max(1, (ng.nx_max + nseg - 1) / nseg);
+        const size_t lds = sc::cascade_lds_bytes(d->K, ng.strip_max);
+        if (lds > 160 * 1024)
+            throw Error{SC_ERR_INVALID, "cascade with " + std::to_string(d->K) +
+                                            " weak classifiers does not fit the kernel's LDS (" +
+                                            std::to_string(lds) + " B)"};
+    }
     d->d_levels.ensure(std::max<size_t>(ng.levels.size(), 1));
     d->d_rows.ensure(std::max<size_t>(ng.rows.size(), 1));
     d->d_proj.ensure(std::max<size_t>(ng.proj.size(), 1));
@@ -336,12 +351,11 @@ void ensure_buffers(sc_detector *d, int n) {
     const Geometry &g = d->geo;
     d->d_table.ensure((size_t)g.tg.frame4 * n);
     d->d_counters.ensure((size_t)n + 1);
-    d->d_visited.ensure(1);
-    if (d->debug) {
-        d->d_dbg_p.ensure((size_t)g.grid * n);
-        d->d_dbg_s.ensure((size_t)g.grid * n);
-        d->d_dbg_v.ensure((size_t)g.grid * n);
-    }
+    d->d_visited.ensure(std::max<size_t>(g.rows.size() * n, 1));
+    d->d_queues.ensure(sc::kXcds * sc::kQueueStride);
+    d->d_st_p.ensure(std::max<size_t>((size_t)g.grid * n, 1));
+    d->d_st_s.ensure(std::max<size_t>((size_t)g.grid * n, 1));
+    if (d->debug) d->d_dbg_v.ensure(std::max<size_t>((size_t)g.grid * n, 1));
 }
 
 void timed_begin(sc_detector *d, hipEvent_t *a) {
@@ -363,7 +377,6 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     ensure_buffers(d, n);
     const Geometry &g = d->geo;
     HIPCHK(hipMemsetAsync(d_counts, 0, sizeof(int) * (n + 1), d->stream));
-    HIPCHK(hipMemsetAsync(d->d_visited.p, 0, sizeof(unsigned long long), d->stream));
 
     sc::RowScanArgs ra{d_frames, (long long)H * stride, stride, d->d_table.p, g.tg};
     hipEvent_t e0 = nullptr;
@@ -377,41 +390,54 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_COLSCAN, e0);
 
-    sc::WindowArgs wa{};
-    wa.table = d->d_table.p;
-    wa.g = g.tg;
-    wa.rows = d->d_rows.p;
-    wa.levels = d->d_levels.p;
-    wa.proj = d->d_proj.p;
-    wa.w = reinterpret_cast<const float4 *>(d->d_w.p);
-    wa.bias = d->d_bias.p;
-    wa.theta = d->d_theta.p;
-    wa.stage_off = d->d_stage_off.p;
-    wa.K = d->K;
-    wa.n_stages = d->S;
-    wa.stride_score = d->prm.stride_score;
-    wa.out = d_out;
-    wa.capacity = capacity;
-    wa.counters = d_counts;
-    wa.visited = d->d_visited.p;
-    if (d->debug) {
-        wa.dbg_p = d->d_dbg_p.p;
-        wa.dbg_s = d->d_dbg_s.p;
-        wa.dbg_v = d->d_dbg_v.p;
-    }
-    wa.grid_per_frame = g.grid;
-    wa.lds_nx = (g.nx_max + 63) & ~63;
-    {   // timing ablations for profiling only (wrong results); never set in production
-        static const char *v = std::getenv("SC_VARIANT");
-        wa.variant = v ? std::atoi(v) : 0;
-    }
     d->last_frames = n;
     if (g.rows.empty()) return;
+
+    sc::CascadeArgs ca{};
+    ca.table = d->d_table.p;
+    ca.g = g.tg;
+    ca.rows = d->d_rows.p;
+    ca.levels = d->d_levels.p;
+    ca.proj = d->d_proj.p;
+    ca.w = reinterpret_cast<const float4 *>(d->d_w.p);
+    ca.bias = d->d_bias.p;
+    ca.theta = d->d_theta.p;
+    ca.stage_off = d->d_stage_off.p;
+    ca.K = d->K;
+    ca.n_stages = d->S;
+    ca.n_rows = (int)g.rows.size();
+    ca.n_frames = n;
+    ca.n_sub = g.n_sub;
+    ca.strip_max = g.strip_max;
+    ca.grid_per_frame = g.grid;
+    ca.queues = d->d_queues.p;
+    ca.st_p = d->d_st_p.p;
+    ca.st_s = d->d_st_s.p;
+    HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kXcds * sc::kQueueStride, d->stream));
     timed_begin(d, &e0);
-    sc::launch_windows(wa, (int)g.rows.size(), n, d->debug, d->stream);
+    sc::launch_cascade(ca, d->device, d->stream);
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_WINDOWS, e0);
-    d->last_frames = n;
+
+    sc::WalkArgs wk{};
+    wk.rows = d->d_rows.p;
+    wk.levels = d->d_levels.p;
+    wk.n_rows = (int)g.rows.size();
+    wk.n_stages = d->S;
+    wk.step = g.step;
+    wk.stride_score = d->prm.stride_score;
+    wk.grid_per_frame = g.grid;
+    wk.st_p = d->d_st_p.p;
+    wk.st_s = d->d_st_s.p;
+    wk.out = d_out;
+    wk.capacity = capacity;
+    wk.counters = d_counts;
+    wk.row_visited = d->d_visited.p;
+    wk.dbg_v = d->debug ? d->d_dbg_v.p : nullptr;
+    timed_begin(d, &e0);
+    sc::launch_walk(wk, n, d->stream);
+    HIPCHK(hipGetLastError());
+    timed_end(d, SC_KERNEL_WALK, e0);
 }
 
 bool rec_less(const sc_det_record &a, const sc_det_record &b) {
@@ -435,10 +461,7 @@ int detect_device_sync(sc_detector *d, const uint8_t *d_frames, int n, int W, in
         enqueue(d, d_frames, n, W, H, stride, d->d_out.p, (int)cap_dev, d->d_counters.p);
         HIPCHK(hipMemcpyAsync(counts.data(), d->d_counters.p, sizeof(int) * (n + 1),
                               hipMemcpyDeviceToHost, d->stream));
-        unsigned long long vis = 0;
-        HIPCHK(hipMemcpyAsync(&vis, d->d_visited.p, sizeof(vis), hipMemcpyDeviceToHost, d->stream));
         HIPCHK(hipStreamSynchronize(d->stream));
-        d->last_visited = (long long)vis;
         if ((size_t)counts[0] <= cap_dev) break;
         cap_dev = (size_t)counts[0];
     }
@@ -632,9 +655,6 @@ int sc_synchronize(sc_detector *d) {
     return guarded([&] {
         if (!d) throw Error{SC_ERR_INVALID, "null detector"};
         HIPCHK(hipStreamSynchronize(d->stream));
-        unsigned long long vis = 0;
-        HIPCHK(hipMemcpy(&vis, d->d_visited.p, sizeof(vis), hipMemcpyDeviceToHost));
-        d->last_visited = (long long)vis;
         return SC_OK;
     });
 }
@@ -646,7 +666,20 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value) {
         case SC_INFO_GRID_WINDOWS: *value = d->geo.grid; break;
         case SC_INFO_ROWS: *value = (int64_t)d->geo.rows.size(); break;
         case SC_INFO_TABLE_PITCH: *value = d->geo.tg.rowp; break;
-        case SC_INFO_VISITED: *value = d->last_visited; break;
+        case SC_INFO_VISITED: {  // sum of the walk kernel's per-row counts
+            return guarded([&] {
+                HIPCHK(hipSetDevice(d->device));
+                HIPCHK(hipStreamSynchronize(d->stream));
+                const size_t n = (size_t)d->last_frames * d->geo.rows.size();
+                std::vector<unsigned> rv(n);
+                if (n) HIPCHK(hipMemcpy(rv.data(), d->d_visited.p, n * sizeof(unsigned),
+                                        hipMemcpyDeviceToHost));
+                long long s = 0;
+                for (unsigned v : rv) s += v;
+                *value = s;
+                return SC_OK;
+            });
+        }
         default: return fail(SC_ERR_INVALID, "unknown info key");
     }
     return SC_OK;
@@ -685,15 +718,20 @@ int sc_debug_dump(sc_detector *d, int what, int frame, void *dst, size_t bytes) 
                 }
             return SC_OK;
         }
-        if (!d->debug) throw Error{SC_ERR_INVALID, "debug records disabled (sc_detector_set_debug)"};
         const size_t n = (size_t)g.grid;
-        if (what == SC_DUMP_GRID_STAGE) {
+        if (n == 0) return SC_OK;
+        if (what == SC_DUMP_GRID_STAGE) {  // the cascade kernel's per-window records
             if (bytes < n * 2) throw Error{SC_ERR_CAPACITY, "dump buffer too small"};
-            HIPCHK(hipMemcpy(dst, d->d_dbg_p.p + n * frame, n * 2, hipMemcpyDeviceToHost));
+            std::vector<int8_t> tmp(n);
+            HIPCHK(hipMemcpy(tmp.data(), d->d_st_p.p + n * frame, n, hipMemcpyDeviceToHost));
+            int16_t *o = static_cast<int16_t *>(dst);
+            for (size_t i = 0; i < n; i++) o[i] = tmp[i];
         } else if (what == SC_DUMP_GRID_SCORE) {
             if (bytes < n * 4) throw Error{SC_ERR_CAPACITY, "dump buffer too small"};
-            HIPCHK(hipMemcpy(dst, d->d_dbg_s.p + n * frame, n * 4, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(dst, d->d_st_s.p + n * frame, n * 4, hipMemcpyDeviceToHost));
         } else if (what == SC_DUMP_GRID_VISIT) {
+            if (!d->debug)
+                throw Error{SC_ERR_INVALID, "visited flags need sc_detector_set_debug before detect"};
             if (bytes < n) throw Error{SC_ERR_CAPACITY, "dump buffer too small"};
             HIPCHK(hipMemcpy(dst, d->d_dbg_v.p + n * frame, n, hipMemcpyDeviceToHost));
         } else {

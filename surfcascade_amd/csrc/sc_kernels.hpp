@@ -1,4 +1,5 @@
-// sc_kernels.hpp -- launch interface of the gfx950 kernels (sc_kernels.hip).
+// sc_kernels.hpp -- launch interface of the gfx950 kernels
+// (sc_integral.hip: rowscan, colscan; sc_windows.hip: cascade, walk).
 //
 // Integral-table layout in HBM ("phase-split"): the reference's table is
 // S[y][x][8 channels] (F256Dat, DenseSURFFeatureExtractor.h:21-25).  Windows
@@ -18,6 +19,9 @@
 #include "surfcascade.h"
 
 namespace sc {
+
+constexpr int kXcds = 8;          // MI355X: 8 XCDs, one L2 each
+constexpr int kQueueStride = 64;  // ints between per-XCD queue words (own 256-B line each)
 
 struct TableGeom {
     int W, H, step;
@@ -55,7 +59,12 @@ struct RowScanArgs {
     TableGeom g;
 };
 
-struct WindowArgs {
+// Cascade kernel: persistent workgroups of 4 independent waves; a task is
+// one strip (1/(8*n_sub) of a row's windows) of one (frame, level, y) row.
+// XCD x serves the strips [x*n_sub, (x+1)*n_sub) of every row from its own
+// queue (steals from the others when empty), so the rows its L2 sees stay in
+// a narrow column band.
+struct CascadeArgs {
     const float4 *table;
     TableGeom g;
     const int2 *rows;  // (level, y)
@@ -66,24 +75,36 @@ struct WindowArgs {
     const float *theta;     // [S]
     const int *stage_off;   // [S+1]
     int K, n_stages;
+    int n_rows, n_frames, n_sub;
+    int strip_max;          // max windows of one strip (LDS sizing)
+    long long grid_per_frame;
+    int *queues;            // [kXcds] task counters, zeroed per launch
+    int8_t *st_p;           // [frame][grid]: stage reached (-1 prefilter reject)
+    float *st_s;            // [frame][grid]: last stage score
+};
+
+// Walk kernel: one wave per (frame, row); the adaptive-stride x chain over
+// the row's per-window results (ObjDetector.cpp:185-217).
+struct WalkArgs {
+    const int2 *rows;
+    const LevelInfo *levels;
+    int n_rows, n_stages, step;
     double stride_score;
+    long long grid_per_frame;
+    const int8_t *st_p;
+    const float *st_s;
     sc_det_record *out;
     int capacity;
     int *counters;  // [0] total, [1+f] per frame
-    unsigned long long *visited;
-    // debug (grid-indexed per frame) -- only written by the debug variant
-    int16_t *dbg_p;
-    float *dbg_s;
-    uint8_t *dbg_v;
-    long long grid_per_frame;
-    int lds_nx;  // windows per row the dynamic LDS is sized for (multiple of 64)
-    int n_rows, n_frames;  // set by launch_windows
-    int variant;           // 0 in production; timing ablations (SC_VARIANT env)
+    unsigned *row_visited;  // [frame][row] windows the x chain visited
+    uint8_t *dbg_v;  // optional [frame][grid] visited flags
 };
 
 void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s);
 void launch_colscan(float4 *table, const TableGeom &g, int n_frames, hipStream_t s);
-void launch_windows(const WindowArgs &a, int n_rows, int n_frames, bool debug, hipStream_t s);
-size_t window_lds_bytes(int nx_max);
+// returns the number of workgroups launched
+int launch_cascade(const CascadeArgs &a, int device, hipStream_t s);
+void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s);
+size_t cascade_lds_bytes(int K, int strip_max);
 
 }  // namespace sc

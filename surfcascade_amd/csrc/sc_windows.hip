@@ -1,0 +1,418 @@
+// sc_windows.hip -- gfx950 (CDNA4) window kernels of the detect path.
+//
+// cascade_kernel: persistent workgroups of 4 independent waves.  Each wave
+// pulls tasks from its XCD's queue; a task is one strip of one (frame, level,
+// row y) row of the stride-`step` window grid (ObjDetector.cpp:178-186).
+// XCD x owns the same column band of every row (sc_kernels.hpp), which keeps
+// the table rows its L2 sees narrow: measured on MI355X, 1080p x 24 levels,
+// L2 hit rate 13% -> 48-71% and beyond-L2 read requests -37..-55% against
+// row-per-wave tasks, where the gathers were capped by fabric bandwidth.
+//   1) prefilter: sum(win) > area*6 (DenseSURFFeatureExtractor.cpp:351-358,
+//      ObjDetector.cpp:188); survivors compacted in x order (__ballot + popc).
+//   2) cascade, stage by stage (ObjDetector.cpp:193-199).  Many survivors:
+//      one lane per survivor, the weak index k wave-uniform, the lane sums its
+//      window's results in weak order in a register (GentleAdaboost.cpp:
+//      255-258).  Few survivors: (survivor, weak) items packed k-major over
+//      the lanes, results through LDS, each survivor's lane adds them in k
+//      order.  Each item is ProjectPatches/GetRectsFromPatch/CalcFeature/
+//      Normalize/LogisticRegression::Predict (:459-484, :360-457,
+//      LogisticRegression.cpp:46-68).  The theta test rejects (:197), the
+//      survivors are compacted again.
+//   3) per-window results (stage reached, last stage score) go to HBM.
+// walk_kernel: one wave per row, the adaptive-stride x walk
+// (ObjDetector.cpp:185-217) over the row's results; visited windows that
+// passed every stage are emitted with score (s + p + 1)/S (:201-212).
+//
+// Every f32/f64 operation is the one the reference performs, in its order;
+// compiled with -ffp-contract=off, IEEE sqrt / division, no fast-math.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cstdint>
+
+#include "sc_kernels.hpp"
+
+namespace sc {
+
+namespace {
+
+#ifndef SC_PPATH_GLOBAL_W
+#define SC_PPATH_GLOBAL_W 0
+#endif
+
+constexpr int kWavesPerWg = 4;
+constexpr int kWalkMaxChunks = 64;  // windows per row <= 4096 (host check)
+constexpr int kCascadeThreads = 64 * kWavesPerWg;
+constexpr int kChunkMin = 40;  // below: pack (survivor, weak) items over lanes
+
+// (TL + BR) - (TR + BL) per lane (DenseSURFFeatureExtractor.cpp:385-412).
+__device__ __forceinline__ float4 box4(float4 tl, float4 br, float4 tr, float4 bl) {
+    float4 r;
+    r.x = (tl.x + br.x) - (tr.x + bl.x);
+    r.y = (tl.y + br.y) - (tr.y + bl.y);
+    r.z = (tl.z + br.z) - (tr.z + bl.z);
+    r.w = (tl.w + br.w) - (tr.w + bl.w);
+    return r;
+}
+
+// c_k = (q0+q1)+(q2+q3); SS = (((eps + c0) + c1) ...) + c7   (:427-433)
+__device__ __forceinline__ float ss_hadd(const float (&f)[32]) {
+    float ss = FLT_EPSILON;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        float q0 = f[4 * k] * f[4 * k], q1 = f[4 * k + 1] * f[4 * k + 1];
+        float q2 = f[4 * k + 2] * f[4 * k + 2], q3 = f[4 * k + 3] * f[4 * k + 3];
+        ss = ss + ((q0 + q1) + (q2 + q3));
+    }
+    return ss;
+}
+
+// The 32 box sums of one projected patch: corners deduplicated on the
+// (GW+1) x (GH+1) corner grid; cell index = row*GW + col (GetRectsFromPatch).
+template <int GW, int GH>
+__device__ __forceinline__ void patch_features(const float4 *__restrict__ T, const ProjPatch &pj,
+                                               int half_off, float (&f)[32]) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const float4 *Th = T + h * half_off;
+        float4 prev[GW + 1], cur[GW + 1];
+#pragma unroll
+        for (int c = 0; c <= GW; c++) prev[c] = Th[pj.row0 + pj.col[c]];
+#pragma unroll
+        for (int r = 0; r < GH; r++) {
+            const int ro = pj.row0 + (r + 1) * pj.rowstep;
+#pragma unroll
+            for (int c = 0; c <= GW; c++) cur[c] = Th[ro + pj.col[c]];
+#pragma unroll
+            for (int c = 0; c < GW; c++) {
+                const float4 v = box4(prev[c], cur[c + 1], prev[c + 1], cur[c]);
+                const int o = 8 * (r * GW + c) + 4 * h;
+                f[o + 0] = v.x;
+                f[o + 1] = v.y;
+                f[o + 2] = v.z;
+                f[o + 3] = v.w;
+            }
+#pragma unroll
+            for (int c = 0; c <= GW; c++) prev[c] = cur[c];
+        }
+    }
+}
+
+// One (window, weak classifier) item: CalcFeature + Normalize + Predict.
+// T points at the window's origin cell (half 0); w4 = w[0..35] (LDS).
+__device__ __forceinline__ float weak_eval(const float4 *__restrict__ T, int half_off,
+                                           const ProjPatch &pj, const float4 *w4, double bias) {
+    float f[32];
+    if (pj.shape == 0) patch_features<2, 2>(T, pj, half_off, f);
+    else if (pj.shape == 1) patch_features<1, 4>(T, pj, half_off, f);
+    else patch_features<4, 1>(T, pj, half_off, f);
+    // Normalize (:417-457): clip at sqrt(SS)*theta, renormalise by 1/sqrt(SS2)
+    const float theta = 0.35355338f;  // 2/sqrt(32.f) (.h:36)
+    const float t = sqrtf(ss_hadd(f)) * theta, nt = -t;
+    // _mm_max_ps(_mm_min_ps(f, t), -t) as one v_med3_f32: identical bits here
+    // because f is a finite box sum (never NaN, never -0) and t > 0 (SS >= eps)
+#pragma unroll
+    for (int i = 0; i < 32; i++) f[i] = __builtin_amdgcn_fmed3f(f[i], nt, t);
+    const float r = 1.0f / sqrtf(ss_hadd(f));
+#pragma unroll
+    for (int i = 0; i < 32; i++) f[i] = f[i] * r;
+    // LogisticRegression::Predict (LogisticRegression.cpp:46-68)
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const float4 wv = w4[i];
+        s0 = wv.x * f[4 * i + 0] + s0;
+        s1 = wv.y * f[4 * i + 1] + s1;
+        s2 = wv.z * f[4 * i + 2] + s2;
+        s3 = wv.w * f[4 * i + 3] + s3;
+    }
+    const float z32 = (s0 + s1) + (s2 + s3);
+    double prob = (double)z32;
+    prob += (double)w4[8].x * bias;
+    prob = 1.0 / (1.0 + exp(-prob));
+    return (float)prob;
+}
+
+__device__ __forceinline__ unsigned long long lanes_below() {
+    return (1ull << (threadIdx.x & 63)) - 1ull;
+}
+
+// Orders LDS traffic between the lanes of ONE wave (a wave's DS instructions
+// execute in order; this only stops the compiler from moving them).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ unsigned xcc_id() {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & (kXcds - 1);
+}
+
+// LDS: weights [K][36] f32 | bias [K] f64 | per wave: st_s, sums f32[SA],
+// P f32[64], st_p i16[SA], surv u16[SA]   (SA = strip_max rounded to 64)
+__host__ __device__ inline size_t wave_scratch_bytes(int SA) { return (size_t)SA * 12 + 256; }
+__host__ __device__ inline size_t model_lds_bytes(int K) { return (size_t)K * 144 + (size_t)K * 8; }
+
+__global__ __launch_bounds__(kCascadeThreads) void cascade_kernel(CascadeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int K = a.K;
+    float4 *Wl = reinterpret_cast<float4 *>(smem);
+    double *Bl = reinterpret_cast<double *>(smem + (size_t)K * 144);
+    for (int i = tid; i < K * 9; i += kCascadeThreads) Wl[i] = a.w[i];
+    for (int i = tid; i < K; i += kCascadeThreads) Bl[i] = a.bias[i];
+    __syncthreads();  // the only workgroup barrier: model staged, waves now independent
+
+    const int SA = (a.strip_max + 63) & ~63;
+    unsigned char *ws = smem + model_lds_bytes(K) + (size_t)wv * wave_scratch_bytes(SA);
+    float *st_s = reinterpret_cast<float *>(ws);
+    float *sums = st_s + SA;
+    float *P = sums + SA;
+    int16_t *st_p = reinterpret_cast<int16_t *>(P + 64);
+    uint16_t *surv = reinterpret_cast<uint16_t *>(st_p + SA);
+
+    const TableGeom g = a.g;
+    const int step = g.step, half_off = g.step * g.Qp;
+    const int n_tasks = a.n_frames * a.n_rows * a.n_sub, nseg = kXcds * a.n_sub;
+    int q = (int)xcc_id(), empty = 0;
+    for (;;) {
+        int t = 0;
+        if (lane == 0) t = atomicAdd(&a.queues[q * kQueueStride], 1);
+        t = __builtin_amdgcn_readfirstlane(t);
+        if (t >= n_tasks) {  // this queue is drained: steal from the next XCD's
+            if (++empty == kXcds) break;
+            q = (q + 1) & (kXcds - 1);
+            continue;
+        }
+        const int rt = t / a.n_sub, sub = t - rt * a.n_sub;
+        const int frame = rt / a.n_rows, row = rt - frame * a.n_rows;
+        const int2 rd = a.rows[row];
+        const LevelInfo L = a.levels[rd.x];
+        const int nx = L.nx, y = rd.y;
+        const int nxs = (nx + nseg - 1) / nseg, j0 = (q * a.n_sub + sub) * nxs;
+        if (j0 >= nx) continue;
+        const int nw = min(nx, j0 + nxs) - j0;
+        // origin cell (phase 0, half 0) of window j0 of this row
+        const float4 *T = a.table + (long long)frame * g.frame4 + (long long)y * g.rowp + j0;
+
+        // 1) prefilter; survivors (local window index u) in x order
+        int nsurv = 0;
+        for (int b = 0; b < nw; b += 64) {
+            const int u = b + lane;
+            bool pass = false;
+            if (u < nw) {
+                const float4 *t0 = T + u;
+                const float4 v = box4(t0[0], t0[L.pre_row + L.pre_col], t0[L.pre_col], t0[L.pre_row]);
+                const float m = (((v.x + v.y) + v.z) + v.w) / 2.0f;  // sum(), :351-358
+                pass = m > L.thr;                                    // ObjDetector.cpp:188
+                st_p[u] = pass ? 0 : -1;
+                st_s[u] = 0.0f;
+            }
+            const unsigned long long mk = __ballot(pass);
+            if (pass) surv[nsurv + __popcll(mk & lanes_below())] = (uint16_t)u;
+            nsurv += __popcll(mk);
+        }
+        wave_sync();
+
+        // 2) cascade, stage by stage over the compacted survivors
+        const ProjPatch *projL = a.proj + (long long)rd.x * K;
+        for (int s = 0; s < a.n_stages && nsurv > 0; s++) {
+            const int off = a.stage_off[s], n = a.stage_off[s + 1] - off;
+            if (nsurv >= kChunkMin) {
+                for (int c = 0; c < nsurv; c += 64) {
+                    const int i = c + lane;
+                    if (i < nsurv) {
+                        const float4 *Tj = T + surv[i];
+                        float sum = 0.0f;
+                        for (int k = 0; k < n; k++) {  // k uniform: parameters via scalar loads
+                            const int gk = off + k;
+                            sum += weak_eval(Tj, half_off, projL[gk], a.w + gk * 9, a.bias[gk]);
+                        }
+                        sums[i] = sum;
+                    }
+                }
+            } else {
+                if (lane < nsurv) sums[lane] = 0.0f;
+                wave_sync();
+                const int items = nsurv * n;
+                const float rcp = 1.0f / (float)nsurv;
+                for (int r = 0; r < items; r += 64) {
+                    const int t2 = r + lane;
+                    if (t2 < items) {
+                        int k = (int)((float)t2 * rcp), i = t2 - k * nsurv;  // k = t2 / nsurv
+                        if (i < 0) { k--; i += nsurv; }
+                        else if (i >= nsurv) { k++; i -= nsurv; }
+                        const int gk = off + k;
+#if SC_PPATH_GLOBAL_W
+                        P[lane] = weak_eval(T + surv[i], half_off, projL[gk], a.w + gk * 9, a.bias[gk]);
+#else
+                        P[lane] = weak_eval(T + surv[i], half_off, projL[gk], Wl + gk * 9, Bl[gk]);
+#endif
+                    }
+                    wave_sync();
+                    if (lane < nsurv) {  // this survivor's items of the round, in k order
+                        const int rend = min(r + 64, items);
+                        const int k0 = (r > lane) ? (r - lane + nsurv - 1) / nsurv : 0;
+                        float acc = sums[lane];
+                        for (int t3 = k0 * nsurv + lane; t3 < rend; t3 += nsurv) acc += P[t3 - r];
+                        sums[lane] = acc;
+                    }
+                    wave_sync();
+                }
+            }
+            wave_sync();
+            // stage decision (GentleAdaboost.cpp:259; ObjDetector.cpp:197) and
+            // in-place order-preserving compaction
+            const float th = a.theta[s];
+            int nn = 0;
+            for (int b = 0; b < nsurv; b += 64) {
+                const int i = b + lane;
+                bool keep = false;
+                int u = 0;
+                if (i < nsurv) {
+                    u = surv[i];
+                    const float sc = sums[i] / (float)n;
+                    st_s[u] = sc;
+                    keep = !((double)sc < (double)th);
+                    st_p[u] = (int16_t)(keep ? s + 1 : s);
+                }
+                const unsigned long long mk = __ballot(keep);
+                wave_sync();
+                if (keep) surv[nn + __popcll(mk & lanes_below())] = (uint16_t)u;
+                nn += __popcll(mk);
+            }
+            nsurv = nn;
+            wave_sync();
+        }
+
+        // 3) per-window results to HBM (coalesced)
+        const long long gi = (long long)frame * a.grid_per_frame + L.grid_base +
+                             (long long)(y / step) * nx + j0;
+        for (int u = lane; u < nw; u += 64) {
+            a.st_p[gi + u] = (int8_t)st_p[u];
+            a.st_s[gi + u] = st_s[u];
+        }
+        wave_sync();
+    }
+}
+
+__global__ __launch_bounds__(64) void walk_kernel(WalkArgs a) {
+    __shared__ uint8_t s_flag[kWalkMaxChunks * 64];  // bit0 skip, bit1 detection
+    const int lane = threadIdx.x;
+    const int frame = blockIdx.x / a.n_rows, row = blockIdx.x - frame * a.n_rows;
+    const int2 rd = a.rows[row];
+    const LevelInfo L = a.levels[rd.x];
+    const int y = rd.y, nx = L.nx, S = a.n_stages;
+    const long long gbase = (long long)frame * a.grid_per_frame + L.grid_base +
+                            (long long)(y / a.step) * nx;
+    const int nch = (nx + 63) >> 6;
+    // pass 1: per-window decisions (independent, unrolled: loads in flight together)
+#pragma unroll 4
+    for (int j = lane; j < nch * 64; j += 64) {
+        uint8_t fl = 1;
+        if (j < nx) {
+            const int p = a.st_p[gbase + j];
+            if (p >= 0) {
+                const double fin = ((double)a.st_s[gbase + j] + p + 1) / S;  // ObjDetector.cpp:201
+                fl = (fin < a.stride_score ? 1 : 0) | (p == S ? 2 : 0);        // :214, :203
+            }
+        }
+        s_flag[j] = fl;
+    }
+    __syncthreads();
+    // pass 2: the x chain, +1 after a good window, +2 after a skip (bad /
+    // prefilter reject / past the row end).  From a landing position p it
+    // visits p, p+2, ... until it lands on a good window q (first q >= p of
+    // p's parity with skip == 0), then continues at q+1: one step per good
+    // window instead of one per visited window.
+    const unsigned long long kEven = 0x5555555555555555ull;
+    int start = 0;
+    unsigned long long nvis = 0;
+    for (int c = 0; c < nch; c++) {
+        const uint8_t fl = s_flag[(c << 6) + lane];
+        const unsigned long long sk = __ballot(fl & 1), dt = __ballot(fl & 2);
+        unsigned long long vis = 0;
+        int pos = start;
+        while (pos < 64) {
+            const unsigned long long par = (pos & 1) ? ~kEven : kEven;
+            const unsigned long long from = ~0ull << pos;
+            const unsigned long long good = ~sk & par & from;
+            if (!good) {
+                vis |= par & from;
+                pos = 64 + (pos & 1);
+                break;
+            }
+            const int q = __builtin_ctzll(good);
+            vis |= par & from & (q == 63 ? ~0ull : ((2ull << q) - 1ull));
+            pos = q + 1;
+        }
+        const int lim = min(64, nx - (c << 6));
+        if (lim < 64) vis &= (1ull << lim) - 1ull;
+        start = pos - 64;
+        nvis += __popcll(vis);
+        const int j = (c << 6) + lane;
+        const bool v = (vis >> lane) & 1ull;
+        if (a.dbg_v && j < nx) a.dbg_v[gbase + j] = v ? 1 : 0;
+        const unsigned long long dm = vis & dt;
+        if (dm) {
+            const int cnt = __popcll(dm);
+            int slot0 = 0;
+            if (lane == 0) {
+                slot0 = atomicAdd(&a.counters[0], cnt);
+                atomicAdd(&a.counters[1 + frame], cnt);
+            }
+            slot0 = __shfl(slot0, 0, 64);
+            if ((dm >> lane) & 1ull) {
+                const int idx = slot0 + __popcll(dm & lanes_below());
+                if (idx < a.capacity) {
+                    sc_det_record rec;
+                    rec.frame = frame;
+                    rec.level = rd.x;
+                    rec.x = j * a.step;
+                    rec.y = y;
+                    rec.w = L.l;
+                    rec.h = L.lh;
+                    rec.stage_reached = S;
+                    rec._pad = 0;
+                    rec.score = ((double)a.st_s[gbase + j] + S + 1) / S;
+                    a.out[idx] = rec;
+                }
+            }
+        }
+    }
+    // per-row count, summed on the host on request: one atomic word hit by
+    // every row (~10^4 per frame) serialises at ~90 adds/us
+    if (lane == 0) a.row_visited[blockIdx.x] = (unsigned)nvis;
+}
+
+}  // namespace
+
+int launch_cascade(const CascadeArgs &a, int device, hipStream_t s) {
+    const int SA = (a.strip_max + 63) & ~63;
+    const size_t lds = model_lds_bytes(a.K) + kWavesPerWg * wave_scratch_bytes(SA);
+    static int cus = 0, dev_cached = -1;
+    if (dev_cached != device) {
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        dev_cached = device;
+    }
+    int per_cu = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cascade_kernel, kCascadeThreads, lds);
+    per_cu = std::max(1, std::min(per_cu, 4));
+    const int grid = std::max(1, cus) * per_cu;
+    hipLaunchKernelGGL(cascade_kernel, dim3(grid), dim3(kCascadeThreads), lds, s, a);
+    return grid;
+}
+
+void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s) {
+    hipLaunchKernelGGL(walk_kernel, dim3(a.n_rows * n_frames), dim3(64), 0, s, a);
+}
+
+size_t cascade_lds_bytes(int K, int strip_max) {
+    return model_lds_bytes(K) + kWavesPerWg * wave_scratch_bytes((strip_max + 63) & ~63);
+}
+
+}  // namespace sc
