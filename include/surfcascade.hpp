@@ -1,0 +1,172 @@
+// surfcascade.hpp -- header-only C++ facade over the C ABI (surfcascade.h),
+// shaped like the reference's in-process API so the detect branch of
+// ObjDetector.cpp can switch with minimal edits:
+//
+//   reference                                   here
+//   Model(string) / Load / Save (Model.h:15-18) surfcascade::Model
+//   CascadeClassifier::stage_classifiers,       surfcascade::CascadeClassifier
+//     GetFittedPatchIndexes (CascadeClassifier.h:28-32)
+//   StageClassifier::theta (StageClassifier.h:24), surfcascade::StageClassifier
+//   LogisticRegression::{patch_index, w}         surfcascade::LogisticRegression
+//   DenseSURFFeatureExtractor::ExtractPatches    surfcascade::ExtractPatches
+//   the scan loop ObjDetector.cpp:160-220        surfcascade::Detector::Detect
+//
+// Errors: Load/Save return EXIT_SUCCESS / EXIT_FAILURE like the reference
+// (message in Model::last_error); Detector throws surfcascade::Error.
+#ifndef SURFCASCADE_HPP
+#define SURFCASCADE_HPP
+
+#include <cstdint>
+#include <cstdlib>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "surfcascade.h"
+
+namespace surfcascade {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+inline void check(int rc) {
+    if (rc < 0) throw Error(rc, sc_last_error());
+}
+
+struct Rect {
+    int x, y, width, height;
+};
+
+struct LogisticRegression {
+    int patch_index = 0;
+    std::vector<float> w;  // 33
+    double bias = 1.0;
+};
+
+struct StageClassifier {
+    float theta = 0.0f;
+    std::vector<LogisticRegression> weak_classifiers;
+    void GetFittedPatchIndexes(std::vector<int> &idx) const {
+        for (const auto &wk : weak_classifiers) idx.push_back(wk.patch_index);
+    }
+};
+
+class CascadeClassifier {
+   public:
+    std::vector<StageClassifier> stage_classifiers;
+
+    void GetFittedPatchIndexes(std::vector<std::vector<int>> &patch_indexes) const {
+        for (const auto &s : stage_classifiers) {
+            std::vector<int> v;
+            s.GetFittedPatchIndexes(v);
+            patch_indexes.push_back(v);
+        }
+    }
+    const sc_model *handle() const { return model_.get(); }
+
+   private:
+    friend class Model;
+    struct Free {
+        void operator()(sc_model *m) const { sc_model_free(m); }
+    };
+    std::shared_ptr<sc_model> model_;
+    void adopt(sc_model *m) {
+        model_.reset(m, Free());
+        stage_classifiers.clear();
+        for (int s = 0; s < sc_model_num_stages(m); s++) {
+            StageClassifier st;
+            int nw = 0;
+            check(sc_model_stage(m, s, &st.theta, &nw));
+            for (int k = 0; k < nw; k++) {
+                LogisticRegression wk;
+                wk.w.resize(33);
+                check(sc_model_weak(m, s, k, &wk.patch_index, wk.w.data(), &wk.bias));
+                st.weak_classifiers.push_back(wk);
+            }
+            stage_classifiers.push_back(st);
+        }
+    }
+};
+
+class Model {
+   public:
+    std::string model_cfg, last_error;
+    explicit Model(std::string cfg) : model_cfg(std::move(cfg)) {}
+
+    int Load(CascadeClassifier &c) {
+        sc_model *m = nullptr;
+        if (sc_model_load(model_cfg.c_str(), &m) != SC_OK) {
+            last_error = sc_last_error();
+            return EXIT_FAILURE;
+        }
+        c.adopt(m);
+        return EXIT_SUCCESS;
+    }
+    int Save(const CascadeClassifier &c) {
+        if (!c.handle() || sc_model_save(c.handle(), model_cfg.c_str()) != SC_OK) {
+            last_error = c.handle() ? sc_last_error() : "cascade not loaded";
+            return EXIT_FAILURE;
+        }
+        return EXIT_SUCCESS;
+    }
+};
+
+inline std::vector<Rect> ExtractPatches(int tmpl_w = 40, int tmpl_h = 40) {
+    int n = sc_extract_patches(tmpl_w, tmpl_h, nullptr, 0);
+    check(n);
+    std::vector<int32_t> r((size_t)n * 4);
+    sc_extract_patches(tmpl_w, tmpl_h, r.data(), n);
+    std::vector<Rect> out(n);
+    for (int i = 0; i < n; i++) out[i] = {r[4 * i], r[4 * i + 1], r[4 * i + 2], r[4 * i + 3]};
+    return out;
+}
+
+inline sc_scan_params DefaultScanParams() {
+    sc_scan_params p;
+    sc_scan_params_default(&p);
+    return p;
+}
+
+// One GPU's detector (device model + buffers + one HIP stream).
+class Detector {
+   public:
+    Detector(const CascadeClassifier &c, const sc_scan_params &p = DefaultScanParams(),
+             int device = 0) {
+        sc_detector *d = nullptr;
+        check(sc_detector_create_from_model(c.handle(), &p, device, &d));
+        det_.reset(d);
+    }
+    // The reference's per-image scan (ObjDetector.cpp:165-220): raw windows
+    // (before groupRectangles) and their scores, sorted by (level, y, x).
+    void Detect(const uint8_t *gray, int w, int h, int stride, std::vector<Rect> &wins,
+                std::vector<double> &scores) {
+        std::vector<sc_window> out(1024);
+        int n = 0;
+        int rc = sc_detect(det_.get(), gray, w, h, stride, out.data(), (int)out.size(), &n);
+        if (rc == SC_ERR_CAPACITY) {
+            out.resize(n);
+            rc = sc_detect(det_.get(), gray, w, h, stride, out.data(), (int)out.size(), &n);
+        }
+        check(rc);
+        wins.clear();
+        scores.clear();
+        for (int i = 0; i < n; i++) {
+            wins.push_back({out[i].x, out[i].y, out[i].w, out[i].h});
+            scores.push_back(out[i].score);
+        }
+    }
+    sc_detector *handle() { return det_.get(); }
+
+   private:
+    struct Free {
+        void operator()(sc_detector *d) const { sc_detector_destroy(d); }
+    };
+    std::unique_ptr<sc_detector, Free> det_;
+};
+
+}  // namespace surfcascade
+
+#endif  // SURFCASCADE_HPP

@@ -1,0 +1,45 @@
+// Drives include/surfcascade.hpp the way ObjDetector.cpp's detect branch would
+// (tests/test_facade.py builds and runs it).
+//   facade_main MODEL.cfg OUT.cfg            -> Load, print fitted patches, Save
+//   facade_main MODEL.cfg OUT.cfg FRAME W H  -> also Detect on a raw u8 frame (GPU)
+#include <cstdio>
+#include <fstream>
+#include <iterator>
+#include <vector>
+
+#include "surfcascade.hpp"
+
+int main(int argc, char **argv) {
+    if (argc < 3) return 2;
+    surfcascade::Model model(argv[1]);
+    surfcascade::CascadeClassifier cascade;
+    if (model.Load(cascade) != EXIT_SUCCESS) {
+        std::fprintf(stderr, "load failed: %s\n", model.last_error.c_str());
+        return 1;
+    }
+    std::vector<std::vector<int>> idx;
+    cascade.GetFittedPatchIndexes(idx);
+    const auto patches = surfcascade::ExtractPatches(40, 40);
+    std::printf("stages %zu patches %zu\n", idx.size(), patches.size());
+    for (size_t s = 0; s < idx.size(); s++)
+        std::printf("stage %zu theta %.9g weak %zu first_patch %d\n", s,
+                    cascade.stage_classifiers[s].theta, idx[s].size(), idx[s][0]);
+    surfcascade::Model out(argv[2]);
+    if (out.Save(cascade) != EXIT_SUCCESS) return 1;
+    if (argc >= 6) {
+        std::ifstream f(argv[3], std::ios::binary);
+        std::vector<uint8_t> img((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        const int w = std::atoi(argv[4]), h = std::atoi(argv[5]);
+        sc_scan_params p = surfcascade::DefaultScanParams();
+        p.n_levels = 3;
+        surfcascade::Detector det(cascade, p, 0);
+        std::vector<surfcascade::Rect> wins;
+        std::vector<double> scores;
+        det.Detect(img.data(), w, h, w, wins, scores);
+        std::printf("detections %zu\n", wins.size());
+        for (size_t i = 0; i < wins.size(); i++)
+            std::printf("%d %d %d %d %.17g\n", wins[i].x, wins[i].y, wins[i].width, wins[i].height,
+                        scores[i]);
+    }
+    return 0;
+}

@@ -1,0 +1,53 @@
+"""The C++ facade (include/surfcascade.hpp) compiles with plain g++ against the
+C-ABI library and round-trips a model; on a GPU it also detects."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import FACE_CFG, ROOT
+
+
+@pytest.fixture(scope="module")
+def facade_bin(tmp_path_factory):
+    import surfcascade_amd as sc
+    lib = sc.library_path()
+    out = str(tmp_path_factory.mktemp("facade") / "facade_main")
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "cpp", "facade_main.cpp"), "-o", out,
+                           "-L", os.path.dirname(lib), "-lsurfcascade",
+                           "-Wl,-rpath," + os.path.dirname(lib)])
+    return out
+
+
+def test_facade_load_save(facade_bin, tmp_path, oracle):
+    out_cfg = tmp_path / "m.cfg"
+    r = subprocess.run([facade_bin, FACE_CFG, str(out_cfg)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    ref = oracle.cascade_from_cfg(open(FACE_CFG).read())
+    lines = r.stdout.splitlines()
+    assert lines[0] == "stages %d patches 608" % ref.n_stages
+    for s in range(ref.n_stages):
+        assert "weak %d" % ref.n_weak[s] in lines[1 + s]
+        assert np.float32(float(lines[1 + s].split()[3])) == ref.theta[s]
+    assert out_cfg.read_text() == open(FACE_CFG).read()
+
+
+@pytest.mark.gpu
+def test_facade_detect_matches_oracle(facade_bin, tmp_path, oracle):
+    from surfcascade_amd import synth
+    c = oracle.cascade_from_cfg(open(FACE_CFG).read())
+    img = synth.make_frame(640, 480, 2)
+    fp = tmp_path / "frame.u8"
+    img.tofile(fp)
+    r = subprocess.run([facade_bin, FACE_CFG, str(tmp_path / "o.cfg"), str(fp), "640", "480"],
+                       capture_output=True, text=True, env=dict(os.environ))
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    k = [i for i, l in enumerate(lines) if l.startswith("detections")][0]
+    got = [tuple(l.split()) for l in lines[k + 1:]]
+    ref, _ = oracle.detect(oracle.integral(img), c, oracle.Params(n_levels=3))
+    exp = [(str(d["x"]), str(d["y"]), str(d["w"]), str(d["h"]), "%.17g" % d["score"]) for d in ref]
+    assert int(lines[k].split()[1]) == len(ref)
+    assert got == exp
