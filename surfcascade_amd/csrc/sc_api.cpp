@@ -71,6 +71,7 @@ struct Geometry {
     std::vector<sc::LevelInfo> levels;
     std::vector<int2> rows;
     std::vector<sc::ProjPatch> proj;
+    std::vector<sc::TaskDesc> tasks;
 };
 
 }  // namespace
@@ -92,6 +93,7 @@ struct sc_detector {
     DevBuf<sc::LevelInfo> d_levels;
     DevBuf<int2> d_rows;
     DevBuf<sc::ProjPatch> d_proj;
+    DevBuf<sc::TaskDesc> d_tasks;
     // working buffers
     DevBuf<uint8_t> d_frames;
     DevBuf<float4> d_table;
@@ -126,7 +128,7 @@ struct sc_detector {
         }
         for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
         d_w.release(); d_bias.release(); d_theta.release(); d_stage_off.release();
-        d_levels.release(); d_rows.release(); d_proj.release();
+        d_levels.release(); d_rows.release(); d_proj.release(); d_tasks.release();
         d_frames.release(); d_table.release(); d_out.release(); d_counters.release();
         d_visited.release(); d_queues.release(); d_st_p.release(); d_st_s.release();
         d_dbg_v.release();
@@ -256,7 +258,29 @@ void build_geometry(sc_detector *d, int W, int H) {
             throw Error{SC_ERR_INVALID, "cascade with " + std::to_string(d->K) +
                                             " weak classifiers does not fit the kernel's LDS (" +
                                             std::to_string(lds) + " B)"};
+        // one descriptor per (row, strip)
+        ng.tasks.resize(ng.rows.size() * nseg);
+        for (size_t r = 0; r < ng.rows.size(); r++) {
+            const sc::LevelInfo &L = ng.levels[ng.rows[r].x];
+            const int y = ng.rows[r].y, nxs = (L.nx + nseg - 1) / nseg;
+            for (int sgi = 0; sgi < nseg; sgi++) {
+                sc::TaskDesc t{};
+                const int j0 = sgi * nxs;
+                t.nw = std::max(0, std::min(L.nx, j0 + nxs) - j0);
+                t.t_off = y * tg.rowp + j0;
+                t.g_off = (int)(L.grid_base + (long long)(y / ng.step) * L.nx + j0);
+                t.level = ng.rows[r].x;
+                t.thr = L.thr;
+                t.pre_row = L.pre_row;
+                t.pre_col = L.pre_col;
+                ng.tasks[r * nseg + sgi] = t;
+            }
+        }
     }
+    d->d_tasks.ensure(std::max<size_t>(ng.tasks.size(), 1));
+    if (!ng.tasks.empty())
+        HIPCHK(hipMemcpyAsync(d->d_tasks.p, ng.tasks.data(), ng.tasks.size() * sizeof(sc::TaskDesc),
+                              hipMemcpyHostToDevice, d->stream));
     d->d_levels.ensure(std::max<size_t>(ng.levels.size(), 1));
     d->d_rows.ensure(std::max<size_t>(ng.rows.size(), 1));
     d->d_proj.ensure(std::max<size_t>(ng.proj.size(), 1));
@@ -396,6 +420,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     sc::CascadeArgs ca{};
     ca.table = d->d_table.p;
     ca.g = g.tg;
+    ca.tasks = d->d_tasks.p;
     ca.rows = d->d_rows.p;
     ca.levels = d->d_levels.p;
     ca.proj = d->d_proj.p;

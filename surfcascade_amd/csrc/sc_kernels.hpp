@@ -64,9 +64,22 @@ struct RowScanArgs {
 // XCD x serves the strips [x*n_sub, (x+1)*n_sub) of every row from its own
 // queue (steals from the others when empty), so the rows its L2 sees stay in
 // a narrow column band.
+// One strip of one row, precomputed on the host (one load per task).
+struct TaskDesc {
+    int t_off;    // table offset (float4) of the strip's first window: y*rowp + j0
+    int g_off;    // grid index (within a frame) of that window
+    int nw;       // windows in the strip (0: empty strip)
+    int level;
+    float thr;    // prefilter threshold (float)(l*lh)*k   (ObjDetector.cpp:188)
+    int pre_row;  // lh*rowp
+    int pre_col;  // (l%step)*Qp + l/step
+    int pad;
+};
+
 struct CascadeArgs {
     const float4 *table;
     TableGeom g;
+    const TaskDesc *tasks;  // [n_rows][kXcds*n_sub]
     const int2 *rows;  // (level, y)
     const LevelInfo *levels;
     const ProjPatch *proj;  // [n_levels][K]

@@ -40,6 +40,15 @@ namespace {
 #ifndef SC_PPATH_GLOBAL_W
 #define SC_PPATH_GLOBAL_W 0
 #endif
+#ifndef SC_SLOT_PATH
+#define SC_SLOT_PATH 0
+#endif
+#ifndef SC_CASCADE_MIN_WGS  // workgroups per CU the register budget must allow
+#define SC_CASCADE_MIN_WGS 1
+#endif
+#ifndef SC_HALF_BARRIER  // 1: load the second channel half after the first is consumed
+#define SC_HALF_BARRIER 0
+#endif
 
 constexpr int kWavesPerWg = 4;
 constexpr int kWalkMaxChunks = 64;  // windows per row <= 4096 (host check)
@@ -75,6 +84,9 @@ __device__ __forceinline__ void patch_features(const float4 *__restrict__ T, con
                                                int half_off, float (&f)[32]) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
+#if SC_HALF_BARRIER
+        if (h) __builtin_amdgcn_sched_barrier(0);
+#endif
         const float4 *Th = T + h * half_off;
         float4 prev[GW + 1], cur[GW + 1];
 #pragma unroll
@@ -157,7 +169,7 @@ __device__ __forceinline__ unsigned xcc_id() {
 __host__ __device__ inline size_t wave_scratch_bytes(int SA) { return (size_t)SA * 12 + 256; }
 __host__ __device__ inline size_t model_lds_bytes(int K) { return (size_t)K * 144 + (size_t)K * 8; }
 
-__global__ __launch_bounds__(kCascadeThreads) void cascade_kernel(CascadeArgs a) {
+__global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_kernel(CascadeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int K = a.K;
@@ -176,28 +188,52 @@ __global__ __launch_bounds__(kCascadeThreads) void cascade_kernel(CascadeArgs a)
     uint16_t *surv = reinterpret_cast<uint16_t *>(st_p + SA);
 
     const TableGeom g = a.g;
-    const int step = g.step, half_off = g.step * g.Qp;
+    const int half_off = g.step * g.Qp;
     const int n_tasks = a.n_frames * a.n_rows * a.n_sub, nseg = kXcds * a.n_sub;
     int q = (int)xcc_id(), empty = 0;
+    // dequeue: one atomic per task on this XCD's queue word; the next task's
+    // index and descriptor are fetched while the current task runs
+    auto task_index = [&](int t) {  // queue position -> descriptor slot, frame
+        const int rt = t / a.n_sub, sub = t - rt * a.n_sub;
+        const int frame = rt / a.n_rows, row = rt - frame * a.n_rows;
+        return make_int2(row * nseg + q * a.n_sub + sub, frame);
+    };
+    int t = 0;
+    if (lane == 0) t = atomicAdd(&a.queues[q * kQueueStride], 1);
+    t = __builtin_amdgcn_readfirstlane(t);
+    TaskDesc D{};
+    int2 tf = make_int2(0, 0);
+    if (t < n_tasks) {
+        tf = task_index(t);
+        D = a.tasks[tf.x];
+    }
     for (;;) {
-        int t = 0;
-        if (lane == 0) t = atomicAdd(&a.queues[q * kQueueStride], 1);
-        t = __builtin_amdgcn_readfirstlane(t);
         if (t >= n_tasks) {  // this queue is drained: steal from the next XCD's
             if (++empty == kXcds) break;
             q = (q + 1) & (kXcds - 1);
+            t = 0;
+            if (lane == 0) t = atomicAdd(&a.queues[q * kQueueStride], 1);
+            t = __builtin_amdgcn_readfirstlane(t);
+            if (t < n_tasks) {
+                tf = task_index(t);
+                D = a.tasks[tf.x];
+            }
             continue;
         }
-        const int rt = t / a.n_sub, sub = t - rt * a.n_sub;
-        const int frame = rt / a.n_rows, row = rt - frame * a.n_rows;
-        const int2 rd = a.rows[row];
-        const LevelInfo L = a.levels[rd.x];
-        const int nx = L.nx, y = rd.y;
-        const int nxs = (nx + nseg - 1) / nseg, j0 = (q * a.n_sub + sub) * nxs;
-        if (j0 >= nx) continue;
-        const int nw = min(nx, j0 + nxs) - j0;
+        int tn = 0;  // prefetch the next task index
+        if (lane == 0) tn = atomicAdd(&a.queues[q * kQueueStride], 1);
+        const int frame = tf.y;
+        const int nw = D.nw;
+        if (nw <= 0) {  // empty strip (narrow row)
+            t = __builtin_amdgcn_readfirstlane(tn);
+            if (t < n_tasks) {
+                tf = task_index(t);
+                D = a.tasks[tf.x];
+            }
+            continue;
+        }
         // origin cell (phase 0, half 0) of window j0 of this row
-        const float4 *T = a.table + (long long)frame * g.frame4 + (long long)y * g.rowp + j0;
+        const float4 *T = a.table + (long long)frame * g.frame4 + D.t_off;
 
         // 1) prefilter; survivors (local window index u) in x order
         int nsurv = 0;
@@ -206,9 +242,9 @@ __global__ __launch_bounds__(kCascadeThreads) void cascade_kernel(CascadeArgs a)
             bool pass = false;
             if (u < nw) {
                 const float4 *t0 = T + u;
-                const float4 v = box4(t0[0], t0[L.pre_row + L.pre_col], t0[L.pre_col], t0[L.pre_row]);
+                const float4 v = box4(t0[0], t0[D.pre_row + D.pre_col], t0[D.pre_col], t0[D.pre_row]);
                 const float m = (((v.x + v.y) + v.z) + v.w) / 2.0f;  // sum(), :351-358
-                pass = m > L.thr;                                    // ObjDetector.cpp:188
+                pass = m > D.thr;                                    // ObjDetector.cpp:188
                 st_p[u] = pass ? 0 : -1;
                 st_s[u] = 0.0f;
             }
@@ -219,9 +255,42 @@ __global__ __launch_bounds__(kCascadeThreads) void cascade_kernel(CascadeArgs a)
         wave_sync();
 
         // 2) cascade, stage by stage over the compacted survivors
-        const ProjPatch *projL = a.proj + (long long)rd.x * K;
+        const ProjPatch *projL = a.proj + (long long)D.level * K;
         for (int s = 0; s < a.n_stages && nsurv > 0; s++) {
             const int off = a.stage_off[s], n = a.stage_off[s + 1] - off;
+#if SC_SLOT_PATH
+            {
+                // k-parallel slots: lane = (slot g, survivor i).  `slots` weak
+                // classifiers of G = 64/slots survivors run side by side, so a
+                // wave holds only G windows in flight (the L2 footprint of an
+                // XCD shrinks with it); the slot outputs of a survivor are
+                // gathered with shuffles and added in k order.
+                const int slots = n >= 8 ? 8 : 4, lg = n >= 8 ? 3 : 4;  // G = 8 or 16
+                const int G = 1 << lg, g = lane >> lg, li = lane & (G - 1);
+                for (int c = 0; c < nsurv; c += G) {
+                    const int i = c + li;
+                    const bool live = i < nsurv;
+                    const float4 *Tj = T + (live ? surv[i] : 0);
+                    float sum = 0.0f;
+                    for (int kk = 0; kk < n; kk += slots) {
+                        const int k = kk + g;
+                        float p = 0.0f;
+                        if (live && k < n) {
+                            const int gk = off + k;
+                            p = weak_eval(Tj, half_off, projL[gk], Wl + gk * 9, Bl[gk]);
+                        }
+#pragma unroll
+                        for (int gg = 0; gg < 8; gg++) {
+                            if (gg < slots) {
+                                const float v = __shfl(p, (gg << lg) + li, 64);
+                                if (kk + gg < n) sum += v;  // GentleAdaboost.cpp:255-258 order
+                            }
+                        }
+                    }
+                    if (g == 0 && live) sums[i] = sum;
+                }
+            }
+#else
             if (nsurv >= kChunkMin) {
                 for (int c = 0; c < nsurv; c += 64) {
                     const int i = c + lane;
@@ -264,6 +333,7 @@ __global__ __launch_bounds__(kCascadeThreads) void cascade_kernel(CascadeArgs a)
                     wave_sync();
                 }
             }
+#endif
             wave_sync();
             // stage decision (GentleAdaboost.cpp:259; ObjDetector.cpp:197) and
             // in-place order-preserving compaction
@@ -290,13 +360,17 @@ __global__ __launch_bounds__(kCascadeThreads) void cascade_kernel(CascadeArgs a)
         }
 
         // 3) per-window results to HBM (coalesced)
-        const long long gi = (long long)frame * a.grid_per_frame + L.grid_base +
-                             (long long)(y / step) * nx + j0;
+        const long long gi = (long long)frame * a.grid_per_frame + D.g_off;
         for (int u = lane; u < nw; u += 64) {
             a.st_p[gi + u] = (int8_t)st_p[u];
             a.st_s[gi + u] = st_s[u];
         }
         wave_sync();
+        t = __builtin_amdgcn_readfirstlane(tn);
+        if (t < n_tasks) {
+            tf = task_index(t);
+            D = a.tasks[tf.x];
+        }
     }
 }
 
