@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cfloat>
 #include <cstdint>
 
@@ -476,6 +477,8 @@ int launch_cascade(const CascadeArgs &a, int device, hipStream_t s) {
     int per_cu = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cascade_kernel, kCascadeThreads, lds);
     per_cu = std::max(1, std::min(per_cu, 4));
+    if (const char *e = std::getenv("SC_WGS_PER_CU"))  // tuning override
+        per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
     const int grid = std::max(1, cus) * per_cu;
     hipLaunchKernelGGL(cascade_kernel, dim3(grid), dim3(kCascadeThreads), lds, s, a);
     return grid;
