@@ -88,6 +88,8 @@ struct sc_detector {
     DevBuf<double> d_bias;
     DevBuf<float> d_theta;
     DevBuf<int> d_stage_off;
+    DevBuf<int16_t> d_order;      // per stage: weak indices sorted by patch shape
+    int chunk_min = 1 << 30;  // one-lane-per-window stages only when n > item buffer
     // geometry on device
     Geometry geo;
     DevBuf<sc::LevelInfo> d_levels;
@@ -127,7 +129,7 @@ struct sc_detector {
             event_pool.push_back(p.b);
         }
         for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
-        d_w.release(); d_bias.release(); d_theta.release(); d_stage_off.release();
+        d_w.release(); d_bias.release(); d_theta.release(); d_stage_off.release(); d_order.release();
         d_levels.release(); d_rows.release(); d_proj.release(); d_tasks.release();
         d_frames.release(); d_table.release(); d_out.release(); d_counters.release();
         d_visited.release(); d_queues.release(); d_st_p.release(); d_st_s.release();
@@ -322,6 +324,24 @@ void upload_model(sc_detector *d) {
         }
     }
     off[d->S] = g;
+    // Evaluation order of the item path: within each stage, weak classifiers
+    // grouped by patch shape (square / tall / wide, as GetRectsFromPatch splits
+    // them) so a wave instruction mostly sees one shape.  Sums still follow
+    // the model's order.
+    std::vector<int16_t> order(std::max(d->K, 1));
+    auto shape = [&](int k) {
+        const int32_t *r = &d->patch_rects[4 * k];
+        return r[2] == r[3] ? 0 : (r[2] < r[3] ? 1 : 2);
+    };
+    for (int s = 0; s < d->S; s++) {
+        std::vector<int> ks;
+        for (int k = off[s]; k < off[s + 1]; k++) ks.push_back(k - off[s]);
+        std::stable_sort(ks.begin(), ks.end(),
+                         [&](int x, int y) { return shape(off[s] + x) < shape(off[s] + y); });
+        for (size_t j = 0; j < ks.size(); j++) order[off[s] + j] = (int16_t)ks[j];
+    }
+    if (d->K > 32767) throw Error{SC_ERR_MODEL, "more than 32767 weak classifiers"};
+    if (const char *e = std::getenv("SC_CHUNK_MIN")) d->chunk_min = std::max(1, std::atoi(e));
     d->d_w.ensure(w.size());
     d->d_bias.ensure(bias.size());
     d->d_theta.ensure(theta.size());
@@ -330,6 +350,8 @@ void upload_model(sc_detector *d) {
     HIPCHK(hipMemcpy(d->d_bias.p, bias.data(), bias.size() * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d->d_theta.p, theta.data(), theta.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(d->d_stage_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+    d->d_order.ensure(order.size());
+    HIPCHK(hipMemcpy(d->d_order.p, order.data(), order.size() * 2, hipMemcpyHostToDevice));
 }
 
 void check_params(const sc_scan_params &p) {
@@ -428,6 +450,8 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     ca.bias = d->d_bias.p;
     ca.theta = d->d_theta.p;
     ca.stage_off = d->d_stage_off.p;
+    ca.order = d->d_order.p;
+    ca.chunk_min = d->chunk_min;
     ca.K = d->K;
     ca.n_stages = d->S;
     ca.n_rows = (int)g.rows.size();

@@ -87,7 +87,9 @@ struct CascadeArgs {
     const double *bias;     // [K]
     const float *theta;     // [S]
     const int *stage_off;   // [S+1]
+    const int16_t *order;   // [K]: per stage, local weak indices sorted by patch shape
     int K, n_stages;
+    int chunk_min;          // survivors from which a stage runs one lane per window
     int n_rows, n_frames, n_sub;
     int strip_max;          // max windows of one strip (LDS sizing)
     long long grid_per_frame;

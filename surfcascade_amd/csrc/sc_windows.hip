@@ -41,9 +41,6 @@ namespace {
 #ifndef SC_PPATH_GLOBAL_W
 #define SC_PPATH_GLOBAL_W 0
 #endif
-#ifndef SC_SLOT_PATH
-#define SC_SLOT_PATH 0
-#endif
 #ifndef SC_CASCADE_MIN_WGS  // workgroups per CU the register budget must allow
 #define SC_CASCADE_MIN_WGS 1
 #endif
@@ -51,10 +48,14 @@ namespace {
 #define SC_HALF_BARRIER 0
 #endif
 
+#ifndef SC_ITEM_BUF  // per-wave LDS results of the (survivor, weak) item path
+#define SC_ITEM_BUF 640
+#endif
+
 constexpr int kWavesPerWg = 4;
+constexpr int kItemBuf = SC_ITEM_BUF;
 constexpr int kWalkMaxChunks = 64;  // windows per row <= 4096 (host check)
 constexpr int kCascadeThreads = 64 * kWavesPerWg;
-constexpr int kChunkMin = 40;  // below: pack (survivor, weak) items over lanes
 
 // (TL + BR) - (TR + BL) per lane (DenseSURFFeatureExtractor.cpp:385-412).
 __device__ __forceinline__ float4 box4(float4 tl, float4 br, float4 tr, float4 bl) {
@@ -165,19 +166,29 @@ __device__ __forceinline__ unsigned xcc_id() {
     return x & (kXcds - 1);
 }
 
-// LDS: weights [K][36] f32 | bias [K] f64 | per wave: st_s, sums f32[SA],
-// P f32[64], st_p i16[SA], surv u16[SA]   (SA = strip_max rounded to 64)
-__host__ __device__ inline size_t wave_scratch_bytes(int SA) { return (size_t)SA * 12 + 256; }
-__host__ __device__ inline size_t model_lds_bytes(int K) { return (size_t)K * 144 + (size_t)K * 8; }
+// LDS: weights [K][36] f32 | bias [K] f64 | order [K] i16 | per wave: st_s,
+// sums f32[SA], P f32[kItemBuf], st_p i16[SA], surv u16[SA]
+// (SA = strip_max rounded to 64)
+__host__ __device__ inline size_t wave_scratch_bytes(int SA) {
+    return (size_t)SA * 12 + (size_t)kItemBuf * 4;
+}
+constexpr int kLdsWeights = SC_PPATH_GLOBAL_W ? 0 : 1;
+__host__ __device__ inline size_t model_lds_bytes(int K) {
+    return kLdsWeights * ((size_t)K * 144 + (size_t)K * 8) + (((size_t)K * 2 + 15) & ~(size_t)15);
+}
 
 __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_kernel(CascadeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int K = a.K;
     float4 *Wl = reinterpret_cast<float4 *>(smem);
-    double *Bl = reinterpret_cast<double *>(smem + (size_t)K * 144);
-    for (int i = tid; i < K * 9; i += kCascadeThreads) Wl[i] = a.w[i];
-    for (int i = tid; i < K; i += kCascadeThreads) Bl[i] = a.bias[i];
+    double *Bl = reinterpret_cast<double *>(smem + kLdsWeights * (size_t)K * 144);
+    int16_t *Ol = reinterpret_cast<int16_t *>(Bl + kLdsWeights * K);
+    for (int i = tid; i < kLdsWeights * K * 9; i += kCascadeThreads) Wl[i] = a.w[i];
+    for (int i = tid; i < K; i += kCascadeThreads) {
+        if (kLdsWeights) Bl[i] = a.bias[i];
+        Ol[i] = a.order[i];
+    }
     __syncthreads();  // the only workgroup barrier: model staged, waves now independent
 
     const int SA = (a.strip_max + 63) & ~63;
@@ -185,7 +196,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
     float *st_s = reinterpret_cast<float *>(ws);
     float *sums = st_s + SA;
     float *P = sums + SA;
-    int16_t *st_p = reinterpret_cast<int16_t *>(P + 64);
+    int16_t *st_p = reinterpret_cast<int16_t *>(P + kItemBuf);
     uint16_t *surv = reinterpret_cast<uint16_t *>(st_p + SA);
 
     const TableGeom g = a.g;
@@ -259,40 +270,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
         const ProjPatch *projL = a.proj + (long long)D.level * K;
         for (int s = 0; s < a.n_stages && nsurv > 0; s++) {
             const int off = a.stage_off[s], n = a.stage_off[s + 1] - off;
-#if SC_SLOT_PATH
-            {
-                // k-parallel slots: lane = (slot g, survivor i).  `slots` weak
-                // classifiers of G = 64/slots survivors run side by side, so a
-                // wave holds only G windows in flight (the L2 footprint of an
-                // XCD shrinks with it); the slot outputs of a survivor are
-                // gathered with shuffles and added in k order.
-                const int slots = n >= 8 ? 8 : 4, lg = n >= 8 ? 3 : 4;  // G = 8 or 16
-                const int G = 1 << lg, g = lane >> lg, li = lane & (G - 1);
-                for (int c = 0; c < nsurv; c += G) {
-                    const int i = c + li;
-                    const bool live = i < nsurv;
-                    const float4 *Tj = T + (live ? surv[i] : 0);
-                    float sum = 0.0f;
-                    for (int kk = 0; kk < n; kk += slots) {
-                        const int k = kk + g;
-                        float p = 0.0f;
-                        if (live && k < n) {
-                            const int gk = off + k;
-                            p = weak_eval(Tj, half_off, projL[gk], Wl + gk * 9, Bl[gk]);
-                        }
-#pragma unroll
-                        for (int gg = 0; gg < 8; gg++) {
-                            if (gg < slots) {
-                                const float v = __shfl(p, (gg << lg) + li, 64);
-                                if (kk + gg < n) sum += v;  // GentleAdaboost.cpp:255-258 order
-                            }
-                        }
-                    }
-                    if (g == 0 && live) sums[i] = sum;
-                }
-            }
-#else
-            if (nsurv >= kChunkMin) {
+            if (nsurv >= a.chunk_min || n > kItemBuf) {
                 for (int c = 0; c < nsurv; c += 64) {
                     const int i = c + lane;
                     if (i < nsurv) {
@@ -306,35 +284,35 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
                     }
                 }
             } else {
-                if (lane < nsurv) sums[lane] = 0.0f;
-                wave_sync();
-                const int items = nsurv * n;
-                const float rcp = 1.0f / (float)nsurv;
-                for (int r = 0; r < items; r += 64) {
-                    const int t2 = r + lane;
-                    if (t2 < items) {
-                        int k = (int)((float)t2 * rcp), i = t2 - k * nsurv;  // k = t2 / nsurv
-                        if (i < 0) { k--; i += nsurv; }
-                        else if (i >= nsurv) { k++; i -= nsurv; }
-                        const int gk = off + k;
+                // (survivor, weak) items over the lanes, groups of G survivors
+                // whose n*G results fit the wave's LDS buffer.  Items run in
+                // shape-sorted weak order (Ol: few patch shapes per wave
+                // instruction, so little divergence); each survivor's lane then
+                // adds its results in the reference's k order.
+                const int gcap = min(64, kItemBuf / n);
+                for (int c = 0; c < nsurv; c += gcap) {
+                    const int G = min(gcap, nsurv - c), items = G * n;
+                    const float rcp = 1.0f / (float)G;
+                    for (int t2 = lane; t2 < items; t2 += 64) {
+                        int kk = (int)((float)t2 * rcp), i = t2 - kk * G;  // kk = t2 / G
+                        if (i < 0) { kk--; i += G; }
+                        else if (i >= G) { kk++; i -= G; }
+                        const int k = Ol[off + kk], gk = off + k;
 #if SC_PPATH_GLOBAL_W
-                        P[lane] = weak_eval(T + surv[i], half_off, projL[gk], a.w + gk * 9, a.bias[gk]);
+                        P[k * G + i] = weak_eval(T + surv[c + i], half_off, projL[gk], a.w + gk * 9, a.bias[gk]);
 #else
-                        P[lane] = weak_eval(T + surv[i], half_off, projL[gk], Wl + gk * 9, Bl[gk]);
+                        P[k * G + i] = weak_eval(T + surv[c + i], half_off, projL[gk], Wl + gk * 9, Bl[gk]);
 #endif
                     }
                     wave_sync();
-                    if (lane < nsurv) {  // this survivor's items of the round, in k order
-                        const int rend = min(r + 64, items);
-                        const int k0 = (r > lane) ? (r - lane + nsurv - 1) / nsurv : 0;
-                        float acc = sums[lane];
-                        for (int t3 = k0 * nsurv + lane; t3 < rend; t3 += nsurv) acc += P[t3 - r];
-                        sums[lane] = acc;
+                    if (lane < G) {
+                        float acc = 0.0f;  // GentleAdaboost.cpp:255-258 order
+                        for (int k = 0; k < n; k++) acc += P[k * G + lane];
+                        sums[c + lane] = acc;
                     }
                     wave_sync();
                 }
             }
-#endif
             wave_sync();
             // stage decision (GentleAdaboost.cpp:259; ObjDetector.cpp:197) and
             // in-place order-preserving compaction

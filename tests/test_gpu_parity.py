@@ -77,6 +77,20 @@ def test_grid_parity_default_levels_odd_size(sc, oracle, face_cascade):
     _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(), oracle.Params())
 
 
+@pytest.mark.parametrize("chunk_min,substrips", [("1", None), ("40", None), (None, "3")])
+def test_grid_parity_kernel_paths(sc, oracle, face_cascade, monkeypatch, chunk_min, substrips):
+    """The one-lane-per-window stage path (used for stages with more weak
+    classifiers than the item buffer holds) and other strip splits give the
+    same bits as the default item path."""
+    if chunk_min:
+        monkeypatch.setenv("SC_CHUNK_MIN", chunk_min)
+    if substrips:
+        monkeypatch.setenv("SC_SUBSTRIPS", substrips)
+    img = _frame(1280, 720, 77)
+    _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=8),
+                 oracle.Params(n_levels=8))
+
+
 def test_pedestrian_64x128(sc, oracle, ped_cascade):
     img = _frame(960, 540, 21)
     _grid_parity(sc, oracle, ped_cascade, PED_CFG, img,
