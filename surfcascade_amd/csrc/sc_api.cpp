@@ -31,6 +31,9 @@ struct sc_model {
 
 namespace {
 
+constexpr int kBandRows = 1;  // grid rows per cascade task (SC_BAND_ROWS overrides)
+constexpr bool kSplitLayout = true;  // table cell format (SC_TABLE_LAYOUT=0/1 overrides)
+
 thread_local std::string g_err;
 
 int fail(int code, const std::string &msg) {
@@ -65,7 +68,8 @@ struct DevBuf {
 struct Geometry {
     int W = 0, H = 0;
     int n_levels = 0, step = 1, nx_max = 0;
-    int n_sub = 1, strip_max = 1;  // cascade tasks: 8*n_sub strips per row
+    int n_sub = 1, strip_max = 1;  // cascade tasks: 8*n_sub strips per band
+    int band_rows = 1, n_bands = 0;
     sc::TableGeom tg{};
     long long grid = 0;
     std::vector<sc::LevelInfo> levels;
@@ -99,6 +103,7 @@ struct sc_detector {
     // working buffers
     DevBuf<uint8_t> d_frames;
     DevBuf<float4> d_table;
+    DevBuf<uint32_t> d_carry;    // integral pass 1 -> pass 2: per-strip row prefixes
     int table_frames = 0;
     DevBuf<sc_det_record> d_out;
     DevBuf<int> d_counters;
@@ -131,7 +136,7 @@ struct sc_detector {
         for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
         d_w.release(); d_bias.release(); d_theta.release(); d_stage_off.release(); d_order.release();
         d_levels.release(); d_rows.release(); d_proj.release(); d_tasks.release();
-        d_frames.release(); d_table.release(); d_out.release(); d_counters.release();
+        d_frames.release(); d_table.release(); d_carry.release(); d_out.release(); d_counters.release();
         d_visited.release(); d_queues.release(); d_st_p.release(); d_st_s.release();
         d_dbg_v.release();
         if (stream) (void)hipStreamDestroy(stream);
@@ -184,12 +189,16 @@ void build_geometry(sc_detector *d, int W, int H) {
         const int Q = (W + 1 + ng.step - 1) / ng.step;
         t.Qp = (Q + 15) & ~15;
         t.rowp = 2 * ng.step * t.Qp;
+        const char *el = std::getenv("SC_TABLE_LAYOUT");  // tuning override
+        const bool split = el ? std::atoi(el) == 0 : kSplitLayout;
+        t.cs = split ? 1 : 2;
+        t.hs = split ? ng.step * t.Qp : 1;
         t.frame4 = (long long)(H + 1) * t.rowp;
-        if ((long long)(H + 1) * t.rowp > (1ll << 30))
+        if ((long long)(H + 1) * t.rowp > (1ll << 28))  // byte offsets within a frame table: u32
             throw Error{SC_ERR_INVALID, "frame too large for 32-bit table offsets"};
     }
     const sc::TableGeom &tg = ng.tg;
-    auto col_off = [&](int cx) { return (cx % tg.step) * tg.Qp + cx / tg.step; };
+    auto col_off = [&](int cx) { return tg.at(cx, 0); };
     ng.proj.resize((size_t)ng.n_levels * d->K);
     long long gb = 0;
     for (int i = 0; i < ng.n_levels; i++) {
@@ -249,35 +258,46 @@ void build_geometry(sc_detector *d, int W, int H) {
         ng.levels.push_back(L);
     }
     ng.grid = gb;  // may be 0: no window fits (the reference loop runs 0 times)
-    {   // cascade task size: ~72 windows per strip at the widest level
-        const char *e = std::getenv("SC_SUBSTRIPS");  // tuning override
+    {   // cascade tasks: one strip (~72 windows wide at the widest level) of a
+        // band of band_rows consecutive grid rows of one level
+        const char *e = std::getenv("SC_SUBSTRIPS");  // tuning overrides
         ng.n_sub = e ? std::max(1, std::atoi(e))
                      : std::max(1, (ng.nx_max + sc::kXcds * 72 / 2) / (sc::kXcds * 72));
+        const char *eb = std::getenv("SC_BAND_ROWS");
+        ng.band_rows = eb ? std::max(1, std::atoi(eb)) : kBandRows;
         const int nseg = sc::kXcds * ng.n_sub;
         ng.strip_max = std::max(1, (ng.nx_max + nseg - 1) / nseg);
-        const size_t lds = sc::cascade_lds_bytes(d->K, ng.strip_max);
+        if (ng.strip_max > 0xffff) throw Error{SC_ERR_INVALID, "strip too wide"};
+        const size_t lds = sc::cascade_lds_bytes(d->K, ng.strip_max, ng.band_rows);
         if (lds > 160 * 1024)
             throw Error{SC_ERR_INVALID, "cascade with " + std::to_string(d->K) +
                                             " weak classifiers does not fit the kernel's LDS (" +
                                             std::to_string(lds) + " B)"};
-        // one descriptor per (row, strip)
-        ng.tasks.resize(ng.rows.size() * nseg);
-        for (size_t r = 0; r < ng.rows.size(); r++) {
-            const sc::LevelInfo &L = ng.levels[ng.rows[r].x];
-            const int y = ng.rows[r].y, nxs = (L.nx + nseg - 1) / nseg;
+        // one descriptor per (band, strip); rows are level-major, y ascending
+        ng.tasks.clear();
+        for (size_t r0 = 0; r0 < ng.rows.size();) {
+            const int lv = ng.rows[r0].x;
+            size_t r1 = r0;
+            while (r1 < ng.rows.size() && ng.rows[r1].x == lv && (int)(r1 - r0) < ng.band_rows) r1++;
+            const sc::LevelInfo &L = ng.levels[lv];
+            const int y = ng.rows[r0].y, nxs = (L.nx + nseg - 1) / nseg;
             for (int sgi = 0; sgi < nseg; sgi++) {
                 sc::TaskDesc t{};
                 const int j0 = sgi * nxs;
                 t.nw = std::max(0, std::min(L.nx, j0 + nxs) - j0);
-                t.t_off = y * tg.rowp + j0;
+                t.nr = (int)(r1 - r0);
+                t.g_row = L.nx;
+                t.t_off = y * tg.rowp + j0 * tg.cs;
                 t.g_off = (int)(L.grid_base + (long long)(y / ng.step) * L.nx + j0);
-                t.level = ng.rows[r].x;
+                t.level = lv;
                 t.thr = L.thr;
                 t.pre_row = L.pre_row;
                 t.pre_col = L.pre_col;
-                ng.tasks[r * nseg + sgi] = t;
+                ng.tasks.push_back(t);
             }
+            r0 = r1;
         }
+        ng.n_bands = (int)(ng.tasks.size() / nseg);
     }
     d->d_tasks.ensure(std::max<size_t>(ng.tasks.size(), 1));
     if (!ng.tasks.empty())
@@ -396,6 +416,7 @@ sc_detector *make_detector(const sc::Cascade &c, const sc_scan_params *p, int de
 void ensure_buffers(sc_detector *d, int n) {
     const Geometry &g = d->geo;
     d->d_table.ensure((size_t)g.tg.frame4 * n);
+    d->d_carry.ensure((size_t)n * g.H * ((g.W + sc::kStrip - 1) / sc::kStrip) * 8);
     d->d_counters.ensure((size_t)n + 1);
     d->d_visited.ensure(std::max<size_t>(g.rows.size() * n, 1));
     d->d_queues.ensure(sc::kXcds * sc::kQueueStride);
@@ -424,7 +445,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     const Geometry &g = d->geo;
     HIPCHK(hipMemsetAsync(d_counts, 0, sizeof(int) * (n + 1), d->stream));
 
-    sc::RowScanArgs ra{d_frames, (long long)H * stride, stride, d->d_table.p, g.tg};
+    sc::RowScanArgs ra{d_frames, (long long)H * stride, stride, d->d_table.p, g.tg, d->d_carry.p};
     hipEvent_t e0 = nullptr;
     timed_begin(d, &e0);
     sc::launch_rowscan(ra, n, d->stream);
@@ -432,7 +453,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     timed_end(d, SC_KERNEL_ROWSCAN, e0);
 
     timed_begin(d, &e0);
-    sc::launch_colscan(d->d_table.p, g.tg, n, d->stream);
+    sc::launch_colscan(ra, n, d->stream);
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_COLSCAN, e0);
 
@@ -443,8 +464,6 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     ca.table = d->d_table.p;
     ca.g = g.tg;
     ca.tasks = d->d_tasks.p;
-    ca.rows = d->d_rows.p;
-    ca.levels = d->d_levels.p;
     ca.proj = d->d_proj.p;
     ca.w = reinterpret_cast<const float4 *>(d->d_w.p);
     ca.bias = d->d_bias.p;
@@ -454,7 +473,8 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     ca.chunk_min = d->chunk_min;
     ca.K = d->K;
     ca.n_stages = d->S;
-    ca.n_rows = (int)g.rows.size();
+    ca.n_bands = g.n_bands;
+    ca.band_rows = g.band_rows;
     ca.n_frames = n;
     ca.n_sub = g.n_sub;
     ca.strip_max = g.strip_max;
@@ -758,9 +778,9 @@ int sc_debug_dump(sc_detector *d, int what, int frame, void *dst, size_t bytes) 
             float *o = static_cast<float *>(dst);
             for (int y = 0; y <= g.H; y++)
                 for (int x = 0; x <= g.W; x++) {
-                    const size_t base = (size_t)y * t.rowp + x / t.step;
-                    const float4 lo = tab[base + (size_t)(x % t.step) * t.Qp];
-                    const float4 hi = tab[base + (size_t)(t.step + x % t.step) * t.Qp];
+                    const size_t base = (size_t)y * t.rowp + t.at(x, 0);
+                    const float4 lo = tab[base];
+                    const float4 hi = tab[base + t.hs];
                     float *c = o + ((size_t)y * (g.W + 1) + x) * 8;
                     c[0] = lo.x; c[1] = lo.y; c[2] = lo.z; c[3] = lo.w;
                     c[4] = hi.x; c[5] = hi.y; c[6] = hi.z; c[7] = hi.w;

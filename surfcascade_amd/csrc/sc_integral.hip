@@ -1,18 +1,25 @@
 // sc_integral.hip -- gfx950 (CDNA4) integral-table kernels of the detect path.
 //
-//   rowscan  : T2bFilter gradients (DenseSURFFeatureExtractor.cpp:199-349)
-//              fused with the exact integer row prefix of cv::integral
-//              (:73-76); writes R_y[x] (exact in f32) into table row y+1.
-//   colscan  : the f32 column recurrence S[y+1][x] = S[y][x] + R_y[x],
-//              sequential in y per (x, channel) -- the association order of
-//              OpenCV's scalar integral_.
+// The table S[y][x][c] is OpenCV's integral_ of the 8 T2bFilter gradient
+// planes (DenseSURFFeatureExtractor.cpp:73-76, 199-349): the row prefix
+// R_y[x] = sum_{x'<x} g_c(y, x') is an exact integer, the column sum is the
+// f32 recurrence S[y+1][x] = fl(S[y][x] + R_y[x]) taken sequentially in y
+// (SURVEY.md App. A.2).  Two passes, the table written exactly once:
+//   rowcarry : one wave per (frame, row): gradients of the row in strips of
+//              kStrip pixels; exclusive per-strip prefix ("carry") of the 8
+//              channels (u32, exact) -> carry[frame][y][strip][8].  Also
+//              zeroes table row 0 and column 0.
+//   colstrip : one wave per (frame, strip): for y = 0..H-1 the strip's
+//              gradients again, an exact in-strip prefix (wave scan) plus the
+//              carry gives R_y, then S += R_y in f32 -- the reference's
+//              association order -- and one store per table cell.
+// Lane mapping in both: lane = half*32 + column; half 0 owns channels 0-3
+// (dx, dy), half 1 channels 4-7 (du, dv), i.e. one table half-cell (float4).
 //
-// Every f32/f64 operation is the one the reference performs, in its order;
-// the file is compiled with -ffp-contract=off (no FMA contraction), IEEE
-// sqrt / division (hipcc default), no fast-math.  Table layout: sc_kernels.hpp.
+// Every f32 operation is the one the reference performs, in its order;
+// compiled with -ffp-contract=off, no fast-math.  Table layout: sc_kernels.hpp.
 #include <hip/hip_runtime.h>
 
-#include <cfloat>
 #include <cstdint>
 
 #include "sc_kernels.hpp"
@@ -21,188 +28,157 @@ namespace sc {
 
 namespace {
 
-constexpr int kRowThreads = 256;
-constexpr int kRowPx = 4;                      // pixels per thread
-constexpr int kRowSeg = kRowThreads * kRowPx;  // pixels per segment
+#ifndef SC_COL_UNROLL
+#define SC_COL_UNROLL 16
+#endif
+constexpr int kColUnroll = SC_COL_UNROLL;  // rows per colstrip block (two blocks of loads in flight)
 
 __device__ __forceinline__ uint32_t sat_sub(uint32_t a, uint32_t b) { return a > b ? a - b : 0u; }
 
-// ---------------------------------------------------------------------------
-// rowscan: gradients + exact integer row prefix -> table row y+1
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kRowThreads) void rowscan_kernel(RowScanArgs a) {
-    __shared__ uint8_t s_img[3][kRowSeg + 16];
-    __shared__ __attribute__((aligned(16))) float s_out[kRowSeg * 8];
-    __shared__ uint32_t s_wsum[kRowThreads / 64][8];
+// The 4 gradient values of pixel (y, x) in this lane's half (T2bFilter,
+// DenseSURFFeatureExtractor.cpp:224-347), borders clamped.  Returned packed:
+// p0 = g0 | g1 << 16, p1 = g2 | g3 << 16 (strip sums stay < 2^16).
+struct Px4 {
+    uint32_t a, b, c, d;  // the four source bytes this half needs
+};
 
-    const int y = blockIdx.x, frame = blockIdx.y, tid = threadIdx.x;
-    const int lane = tid & 63, wv = tid >> 6;
-    const TableGeom g = a.g;
-    const int W = g.W, H = g.H, step = g.step, Qp = g.Qp;
-    const uint8_t *img = a.frames + (long long)frame * a.frame_bytes;
-    const uint8_t *rows[3] = {img + (long long)(y > 0 ? y - 1 : 0) * a.stride,
-                              img + (long long)y * a.stride,
-                              img + (long long)(y < H - 1 ? y + 1 : H - 1) * a.stride};
-    float4 *tab = a.table + (long long)frame * g.frame4;
-    float4 *out = tab + (long long)(y + 1) * g.rowp;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-
-    if (y == 0)  // table row 0 is all zeros
-        for (int i = tid; i < g.rowp; i += kRowThreads) tab[i] = z4;
-    if (tid == 0) {  // column 0 (phase 0, q 0) of this row
-        out[0] = z4;
-        out[(long long)step * Qp] = z4;
+__device__ __forceinline__ Px4 load_px(const uint8_t *img, int stride, int W, int H, int y, int x,
+                                       int h) {
+    const int xp = x > 0 ? x - 1 : 0, xn = x < W - 1 ? x + 1 : W - 1;
+    const uint8_t *rc = img + (long long)y * stride;
+    const uint8_t *ru = img + (long long)(y > 0 ? y - 1 : 0) * stride;
+    const uint8_t *rd = img + (long long)(y < H - 1 ? y + 1 : H - 1) * stride;
+    Px4 v;
+    if (h == 0) {  // dx: I[y][x-1], I[y][x+1]; dy: I[y-1][x], I[y+1][x]
+        v.a = rc[xp]; v.b = rc[xn]; v.c = ru[x]; v.d = rd[x];
+    } else {       // du: I[y-1][x-1], I[y+1][x+1]; dv: I[y+1][x-1], I[y-1][x+1]
+        v.a = ru[xp]; v.b = rd[xn]; v.c = rd[xp]; v.d = ru[xn];
     }
+    return v;
+}
 
-    uint32_t carry[8];
-#pragma unroll
-    for (int c = 0; c < 8; c++) carry[c] = 0;
+// plane 2k = sat(Ip - In), plane 2k+1 = sat(In - Ip)  
+__device__ __forceinline__ uint2 grad_packed(const Px4 &v) {
+    // half 0: (Ip, In) = (I[y][x-1], I[y][x+1]) and (I[y-1][x], I[y+1][x])
+    // half 1: (Ip, In) = (I[y-1][x-1], I[y+1][x+1]) and (I[y+1][x-1], I[y-1][x+1])
+    const uint32_t g0 = sat_sub(v.a, v.b), g1 = sat_sub(v.b, v.a);
+    const uint32_t g2 = sat_sub(v.c, v.d), g3 = sat_sub(v.d, v.c);
+    return make_uint2(g0 | (g1 << 16), g2 | (g3 << 16));
+}
 
-    for (int seg = 0; seg < W; seg += kRowSeg) {
-        // stage the three source rows of this segment (x = seg-1 .. seg+kRowSeg)
-        for (int i = tid; i < kRowSeg + 2; i += kRowThreads) {
-            int x = seg - 1 + i;
-            x = x < 0 ? 0 : (x > W - 1 ? W - 1 : x);
-#pragma unroll
-            for (int r = 0; r < 3; r++) s_img[r][i] = rows[r][x];
-        }
-        __syncthreads();
+// inclusive prefix sum within each 32-lane half: DPP row shifts (Hillis-
+// Steele in 16-lane rows), then row 0's / row 2's last lane broadcast into
+// rows 1 / 3 -- VALU only, no LDS round trips
+__device__ __forceinline__ uint32_t half_scan(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    return v;
+}
 
-        const int x0 = seg + tid * kRowPx;
-        uint32_t pre[kRowPx][8];  // inclusive in-thread prefix [px][ch]
-        uint32_t acc[8];
+__global__ __launch_bounds__(64) void rowcarry_kernel(RowScanArgs a) {
+    const int y = blockIdx.x, frame = blockIdx.y, lane = threadIdx.x;
+    const int h = lane >> 5, c = lane & 31;
+    const TableGeom g = a.g;
+    const int W = g.W, H = g.H, ns = (W + kStrip - 1) / kStrip;
+    const uint8_t *img = a.frames + (long long)frame * a.frame_bytes;
+    float4 *tab = a.table + (long long)frame * g.frame4;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (y == 0)  // table row 0 is all zeros
+        for (int i = lane; i < g.rowp; i += 64) tab[i] = z4;
+    if (lane < 2) tab[(long long)(y + 1) * g.rowp + lane * g.hs] = z4;  // column 0
+
+    uint4 *out = reinterpret_cast<uint4 *>(a.carry) + ((long long)frame * H + y) * ns * 2 + h;
+    uint32_t run[4] = {0u, 0u, 0u, 0u};
+    constexpr int kB = 4;  // strips whose pixel loads are in flight together
+    for (int s0 = 0; s0 < ns; s0 += kB) {
+        Px4 px[kB];
 #pragma unroll
-        for (int c = 0; c < 8; c++) acc[c] = 0;
-#pragma unroll
-        for (int px = 0; px < kRowPx; px++) {
-            const int x = x0 + px;
-            if (x < W) {
-                const int xn = (x < W - 1 ? x + 1 : W - 1) - seg + 1;
-                const int xp = (x > 0 ? x - 1 : 0) - seg + 1;
-                const int xc = x - seg + 1;
-                const uint32_t u_c = s_img[0][xc], d_c = s_img[2][xc];
-                const uint32_t c_n = s_img[1][xn], c_p = s_img[1][xp];
-                const uint32_t u_n = s_img[0][xn], u_p = s_img[0][xp];
-                const uint32_t d_n = s_img[2][xn], d_p = s_img[2][xp];
-                acc[0] += sat_sub(c_p, c_n);  // dx: In = I[y][x+1], Ip = I[y][x-1]
-                acc[1] += sat_sub(c_n, c_p);
-                acc[2] += sat_sub(u_c, d_c);  // dy: In = I[y+1][x], Ip = I[y-1][x]
-                acc[3] += sat_sub(d_c, u_c);
-                acc[4] += sat_sub(u_p, d_n);  // du: In = I[y+1][x+1], Ip = I[y-1][x-1]
-                acc[5] += sat_sub(d_n, u_p);
-                acc[6] += sat_sub(d_p, u_n);  // dv: In = I[y-1][x+1], Ip = I[y+1][x-1]
-                acc[7] += sat_sub(u_n, d_p);
-            }
-#pragma unroll
-            for (int c = 0; c < 8; c++) pre[px][c] = acc[c];
-        }
-        // exclusive scan of the per-thread totals across the workgroup (exact ints)
-        uint32_t incl[8];
-#pragma unroll
-        for (int c = 0; c < 8; c++) incl[c] = acc[c];
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-#pragma unroll
-            for (int c = 0; c < 8; c++) {
-                uint32_t v = __shfl_up(incl[c], off, 64);
-                if (lane >= off) incl[c] += v;
-            }
-        }
-        if (lane == 63)
-#pragma unroll
-            for (int c = 0; c < 8; c++) s_wsum[wv][c] = incl[c];
-        __syncthreads();
-        uint32_t base[8], seg_total[8];
-#pragma unroll
-        for (int c = 0; c < 8; c++) {
-            uint32_t b = 0, t = 0;
-#pragma unroll
-            for (int w = 0; w < kRowThreads / 64; w++) {
-                if (w < wv) b += s_wsum[w][c];
-                t += s_wsum[w][c];
-            }
-            base[c] = carry[c] + b + incl[c] - acc[c];
-            seg_total[c] = t;
-        }
-        // R values (exact integers < 2^24, exact in f32) staged in LDS
-#pragma unroll
-        for (int px = 0; px < kRowPx; px++) {
-            float4 lo, hi;
-            lo.x = (float)(base[0] + pre[px][0]);
-            lo.y = (float)(base[1] + pre[px][1]);
-            lo.z = (float)(base[2] + pre[px][2]);
-            lo.w = (float)(base[3] + pre[px][3]);
-            hi.x = (float)(base[4] + pre[px][4]);
-            hi.y = (float)(base[5] + pre[px][5]);
-            hi.z = (float)(base[6] + pre[px][6]);
-            hi.w = (float)(base[7] + pre[px][7]);
-            float4 *d = reinterpret_cast<float4 *>(s_out + (tid * kRowPx + px) * 8);
-            d[0] = lo;
-            d[1] = hi;
-        }
-        __syncthreads();
-        // phase-split stores: cell X = seg+1+i -> (X % step, X / step)
-        for (int i = tid; i < kRowSeg; i += kRowThreads) {
-            const int X = seg + 1 + i;
-            if (X <= W) {
-                const int q = X / step, p = X - q * step;
-                const float4 *src = reinterpret_cast<const float4 *>(s_out + i * 8);
-                out[(long long)p * Qp + q] = src[0];
-                out[(long long)(step + p) * Qp + q] = src[1];
-            }
+        for (int k = 0; k < kB; k++) {
+            const int x = min((s0 + k) * kStrip + c, W - 1);
+            px[k] = load_px(img, a.stride, W, H, y, x, h);
         }
 #pragma unroll
-        for (int c = 0; c < 8; c++) carry[c] += seg_total[c];
-        __syncthreads();
+        for (int k = 0; k < kB; k++) {
+            const int s = s0 + k;
+            if (s >= ns) break;
+            uint2 p = (s * kStrip + c < W) ? grad_packed(px[k]) : make_uint2(0u, 0u);
+            // strip totals of each 32-lane half: its scan's last lane
+            p.x = half_scan(p.x);
+            p.y = half_scan(p.y);
+            const uint32_t tx = h ? __builtin_amdgcn_readlane(p.x, 63) : __builtin_amdgcn_readlane(p.x, 31);
+            const uint32_t ty = h ? __builtin_amdgcn_readlane(p.y, 63) : __builtin_amdgcn_readlane(p.y, 31);
+            if (c == 0) out[(long long)s * 2] = make_uint4(run[0], run[1], run[2], run[3]);
+            run[0] += tx & 0xffffu;
+            run[1] += tx >> 16;
+            run[2] += ty & 0xffffu;
+            run[3] += ty >> 16;
+        }
     }
 }
 
-// ---------------------------------------------------------------------------
-// colscan: S[y+1][x] = fl(S[y][x] + R_y[x]), sequential in y (in place)
-// ---------------------------------------------------------------------------
-constexpr int kColBlk = 32;
-
-__global__ __launch_bounds__(64) void colscan_kernel(float *table, TableGeom g) {
-    const int fi = blockIdx.x * 64 + threadIdx.x;  // float index within a row
-    if (fi >= g.rowp * 4) return;
-    {   // skip padding cells (x > W) -- never written, never read
-        const int f4 = fi >> 2, plane = f4 / g.Qp, q = f4 - plane * g.Qp;
-        const int p = plane % g.step;
-        if (q * g.step + p > g.W) return;
-    }
-    const long long pitch = (long long)g.rowp * 4;
-    const int H = g.H;
-    float *col = table + (long long)blockIdx.y * g.frame4 * 4 + fi;
-    float acc = 0.0f;  // row 0
-    float cur[kColBlk], nxt[kColBlk];
+__global__ __launch_bounds__(64) void colstrip_kernel(RowScanArgs a) {
+    const int s = blockIdx.x, frame = blockIdx.y, lane = threadIdx.x;
+    const int h = lane >> 5, c = lane & 31;
+    const TableGeom g = a.g;
+    const int W = g.W, H = g.H, ns = (W + kStrip - 1) / kStrip;
+    const int x = s * kStrip + c;
+    const bool live = x < W;
+    const int xs = live ? x : W - 1;  // dead lanes still join the scan with zeros
+    const uint8_t *img = a.frames + (long long)frame * a.frame_bytes;
+    float4 *cellp = a.table + (long long)frame * g.frame4 + g.at(x + 1, h);  // row 0 of the column
+    const uint4 *cin = reinterpret_cast<const uint4 *>(a.carry) + (long long)frame * H * ns * 2 +
+                       (long long)s * 2 + h;
+    // software pipeline: the loads of block b+1 are in flight while block b
+    // is scanned and stored
+    Px4 pa[kColUnroll];
+    uint4 ca[kColUnroll];
+    auto load_block = [&](int y0, Px4 (&px)[kColUnroll], uint4 (&cr)[kColUnroll]) {
 #pragma unroll
-    for (int k = 0; k < kColBlk; k++) cur[k] = (1 + k <= H) ? col[(1 + k) * pitch] : 0.0f;
-    for (int y = 1; y <= H; y += kColBlk) {
-        const int yn = y + kColBlk;
+        for (int k = 0; k < kColUnroll; k++) {
+            const int y = min(y0 + k, H - 1);
+            px[k] = load_px(img, a.stride, W, H, y, xs, h);
+            cr[k] = cin[(long long)y * ns * 2];
+        }
+    };
+    load_block(0, pa, ca);
+    float S0 = 0.0f, S1 = 0.0f, S2 = 0.0f, S3 = 0.0f;  // table row 0
+    for (int y0 = 0; y0 < H; y0 += kColUnroll) {
+        Px4 pb[kColUnroll];
+        uint4 cb[kColUnroll];
+        load_block(y0 + kColUnroll < H ? y0 + kColUnroll : y0, pb, cb);
 #pragma unroll
-        for (int k = 0; k < kColBlk; k++) nxt[k] = (yn + k <= H) ? col[(yn + k) * pitch] : 0.0f;
-#pragma unroll
-        for (int k = 0; k < kColBlk; k++) {
-            if (y + k <= H) {
-                acc = acc + cur[k];
-                col[(y + k) * pitch] = acc;
-            }
+        for (int k = 0; k < kColUnroll; k++) {
+            const int y = y0 + k;  // rows past H: harmless extra steps, not stored
+            uint2 p = live ? grad_packed(pa[k]) : make_uint2(0u, 0u);
+            p.x = half_scan(p.x);
+            p.y = half_scan(p.y);
+            // R_y[x+1] exact (< 2^24), then the f32 column step
+            S0 = S0 + (float)(ca[k].x + (p.x & 0xffffu));
+            S1 = S1 + (float)(ca[k].y + (p.x >> 16));
+            S2 = S2 + (float)(ca[k].z + (p.y & 0xffffu));
+            S3 = S3 + (float)(ca[k].w + (p.y >> 16));
+            if (live && y < H) cellp[(long long)(y + 1) * g.rowp] = make_float4(S0, S1, S2, S3);
         }
 #pragma unroll
-        for (int k = 0; k < kColBlk; k++) cur[k] = nxt[k];
+        for (int k = 0; k < kColUnroll; k++) {
+            pa[k] = pb[k];
+            ca[k] = cb[k];
+        }
     }
 }
 
 }  // namespace
 
 void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
-    hipLaunchKernelGGL(rowscan_kernel, dim3(a.g.H, n_frames), dim3(kRowThreads), 0, s, a);
+    hipLaunchKernelGGL(rowcarry_kernel, dim3(a.g.H, n_frames), dim3(64), 0, s, a);
 }
 
-void launch_colscan(float4 *table, const TableGeom &g, int n_frames, hipStream_t s) {
-    const int n = g.rowp * 4;
-    hipLaunchKernelGGL(colscan_kernel, dim3((n + 63) / 64, n_frames), dim3(64), 0, s,
-                       reinterpret_cast<float *>(table), g);
+void launch_colscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
+    const int ns = (a.g.W + kStrip - 1) / kStrip;
+    hipLaunchKernelGGL(colstrip_kernel, dim3(ns, n_frames), dim3(64), 0, s, a);
 }
 
 }  // namespace sc

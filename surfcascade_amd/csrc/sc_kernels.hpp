@@ -5,11 +5,14 @@
 // S[y][x][8 channels] (F256Dat, DenseSURFFeatureExtractor.h:21-25).  Windows
 // of one row sit at x = step*j, so the corner a weak classifier reads for
 // window j is at x = step*j + off: always the same phase off % step.  We store
-// each table row as 2 halves (channels 0-3, 4-7) x `step` phase planes x Qp
-// float4 cells:   cell(y, x, half) = y*rowp + (half*step + x%step)*Qp + x/step
-// so lanes working on consecutive windows read consecutive float4s (1 KiB per
-// wave instruction).  Values are bit-identical to the reference table; only
-// the addressing differs (sc_debug_dump converts back).
+// each table row as `step` phase planes of Qp cells, so consecutive windows
+// read consecutive cells.  Two cell formats (TableGeom::cs/hs):
+//   interleaved (cs 2): a cell is 32 B, channels 0-7 together
+//       float4 (y, x, half) = y*rowp + 2*((x%step)*Qp + x/step) + half
+//   channel-split (cs 1): halves (channels 0-3 | 4-7) in separate planes
+//       float4 (y, x, half) = y*rowp + (half*step + x%step)*Qp + x/step
+// Values are bit-identical to the reference table; only the addressing
+// differs (sc_debug_dump converts back).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -25,9 +28,15 @@ constexpr int kQueueStride = 64;  // ints between per-XCD queue words (own 256-B
 
 struct TableGeom {
     int W, H, step;
-    int Qp;    // float4 cells per phase plane (>= ceil((W+1)/step), multiple of 16)
+    int Qp;    // cells per phase plane (>= ceil((W+1)/step), multiple of 16)
     int rowp;  // float4 per table row = 2*step*Qp
+    int cs;    // float4 per cell step: 1 (channel-split halves) or 2 (8 channels together)
+    int hs;    // float4 from a cell's channels 0-3 to its channels 4-7: step*Qp or 1
     long long frame4;  // float4 per frame table = (H+1)*rowp
+    // float4 index of (x, half) within a table row
+    __host__ __device__ int at(int x, int h) const {
+        return cs * ((x % step) * Qp + x / step) + h * hs;
+    }
 };
 
 // One scale level of the window pyramid (ObjDetector.cpp:178-182).
@@ -51,37 +60,40 @@ struct ProjPatch {
     int col[5];   // ((dx+i*c)%step)*Qp + (dx+i*c)/step, i = 0..gw
 };
 
+constexpr int kStrip = 32;  // integral passes: pixels per strip (per 32-lane half wave)
+
 struct RowScanArgs {
     const uint8_t *frames;
     long long frame_bytes;  // distance between frames
     int stride;             // bytes per image row
     float4 *table;
     TableGeom g;
+    uint32_t *carry;        // [frame][H][ceil(W/kStrip)][8] exclusive strip prefixes
 };
 
 // Cascade kernel: persistent workgroups of 4 independent waves; a task is
-// one strip (1/(8*n_sub) of a row's windows) of one (frame, level, y) row.
-// XCD x serves the strips [x*n_sub, (x+1)*n_sub) of every row from its own
-// queue (steals from the others when empty), so the rows its L2 sees stay in
-// a narrow column band.
-// One strip of one row, precomputed on the host (one load per task).
+// one strip (1/(8*n_sub) of a row's windows) of a band of up to band_rows
+// consecutive grid rows of one (frame, level).  XCD x serves the strips
+// [x*n_sub, (x+1)*n_sub) of every band from its own queue (steals from the
+// others when empty), so the rows its L2 sees stay in a narrow column band.
+// One strip of one band, precomputed on the host (one load per task).
 struct TaskDesc {
     int t_off;    // table offset (float4) of the strip's first window: y*rowp + j0
     int g_off;    // grid index (within a frame) of that window
-    int nw;       // windows in the strip (0: empty strip)
+    int nw;       // windows per row of the strip (0: empty strip)
+    int nr;       // grid rows in the band
+    int g_row;    // grid index distance between the band's rows (= level nx)
     int level;
     float thr;    // prefilter threshold (float)(l*lh)*k   (ObjDetector.cpp:188)
     int pre_row;  // lh*rowp
     int pre_col;  // (l%step)*Qp + l/step
-    int pad;
+    int pad[3];
 };
 
 struct CascadeArgs {
     const float4 *table;
     TableGeom g;
-    const TaskDesc *tasks;  // [n_rows][kXcds*n_sub]
-    const int2 *rows;  // (level, y)
-    const LevelInfo *levels;
+    const TaskDesc *tasks;  // [n_bands][kXcds*n_sub]
     const ProjPatch *proj;  // [n_levels][K]
     const float4 *w;        // [K][9]: w[0..32] + 3 pad
     const double *bias;     // [K]
@@ -90,8 +102,9 @@ struct CascadeArgs {
     const int16_t *order;   // [K]: per stage, local weak indices sorted by patch shape
     int K, n_stages;
     int chunk_min;          // survivors from which a stage runs one lane per window
-    int n_rows, n_frames, n_sub;
-    int strip_max;          // max windows of one strip (LDS sizing)
+    int n_bands, n_frames, n_sub;
+    int strip_max;          // max windows per row of one strip (LDS sizing)
+    int band_rows;          // max grid rows per band
     long long grid_per_frame;
     int *queues;            // [kXcds] task counters, zeroed per launch
     int8_t *st_p;           // [frame][grid]: stage reached (-1 prefilter reject)
@@ -115,11 +128,12 @@ struct WalkArgs {
     uint8_t *dbg_v;  // optional [frame][grid] visited flags
 };
 
+// integral pass 1 (rowcarry) and pass 2 (colstrip), sc_integral.hip
 void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s);
-void launch_colscan(float4 *table, const TableGeom &g, int n_frames, hipStream_t s);
+void launch_colscan(const RowScanArgs &a, int n_frames, hipStream_t s);
 // returns the number of workgroups launched
 int launch_cascade(const CascadeArgs &a, int device, hipStream_t s);
 void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s);
-size_t cascade_lds_bytes(int K, int strip_max);
+size_t cascade_lds_bytes(int K, int strip_max, int band_rows);
 
 }  // namespace sc

@@ -44,6 +44,9 @@ namespace {
 #ifndef SC_CASCADE_MIN_WGS  // workgroups per CU the register budget must allow
 #define SC_CASCADE_MIN_WGS 1
 #endif
+#ifndef SC_SADDR  // 1: corner loads as SGPR base + 32-bit VGPR offset
+#define SC_SADDR 1
+#endif
 #ifndef SC_HALF_BARRIER  // 1: load the second channel half after the first is consumed
 #define SC_HALF_BARRIER 0
 #endif
@@ -79,25 +82,41 @@ __device__ __forceinline__ float ss_hadd(const float (&f)[32]) {
     return ss;
 }
 
+// A window's view of the table: uniform base (SGPRs) + the lane's 32-bit
+// byte offset of its origin cell, so each corner load is one
+// `global_load_dwordx4 v, v_off, s[base]` with a single offset VGPR (frame
+// tables are < 4 GiB; host check) instead of a 64-bit per-lane address.
+struct TabView {
+    const char *base;
+    unsigned off;
+    __device__ __forceinline__ float4 at(int cell) const {
+#if SC_SADDR
+        return *reinterpret_cast<const float4 *>(base + (off + ((unsigned)cell << 4)));
+#else
+        return reinterpret_cast<const float4 *>(base + off)[cell];
+#endif
+    }
+};
+
 // The 32 box sums of one projected patch: corners deduplicated on the
 // (GW+1) x (GH+1) corner grid; cell index = row*GW + col (GetRectsFromPatch).
 template <int GW, int GH>
-__device__ __forceinline__ void patch_features(const float4 *__restrict__ T, const ProjPatch &pj,
+__device__ __forceinline__ void patch_features(const TabView &T, const ProjPatch &pj,
                                                int half_off, float (&f)[32]) {
 #pragma unroll
     for (int h = 0; h < 2; h++) {
 #if SC_HALF_BARRIER
         if (h) __builtin_amdgcn_sched_barrier(0);
 #endif
-        const float4 *Th = T + h * half_off;
+        const int ho = h * half_off;
         float4 prev[GW + 1], cur[GW + 1];
 #pragma unroll
-        for (int c = 0; c <= GW; c++) prev[c] = Th[pj.row0 + pj.col[c]];
+        for (int c = 0; c <= GW; c++) prev[c] = T.at(ho + pj.row0 + pj.col[c]);
 #pragma unroll
         for (int r = 0; r < GH; r++) {
-            const int ro = pj.row0 + (r + 1) * pj.rowstep;
+            const int ro = ho + pj.row0 + (r + 1) * pj.rowstep;
 #pragma unroll
-            for (int c = 0; c <= GW; c++) cur[c] = Th[ro + pj.col[c]];
+            for (int c = 0; c <= GW; c++) cur[c] = T.at(ro + pj.col[c]);
 #pragma unroll
             for (int c = 0; c < GW; c++) {
                 const float4 v = box4(prev[c], cur[c + 1], prev[c + 1], cur[c]);
@@ -114,8 +133,8 @@ __device__ __forceinline__ void patch_features(const float4 *__restrict__ T, con
 }
 
 // One (window, weak classifier) item: CalcFeature + Normalize + Predict.
-// T points at the window's origin cell (half 0); w4 = w[0..35] (LDS).
-__device__ __forceinline__ float weak_eval(const float4 *__restrict__ T, int half_off,
+// T views the window's origin cell (half 0); w4 = w[0..35] (LDS).
+__device__ __forceinline__ float weak_eval(const TabView &T, int half_off,
                                            const ProjPatch &pj, const float4 *w4, double bias) {
     float f[32];
     if (pj.shape == 0) patch_features<2, 2>(T, pj, half_off, f);
@@ -144,6 +163,9 @@ __device__ __forceinline__ float weak_eval(const float4 *__restrict__ T, int hal
     const float z32 = (s0 + s1) + (s2 + s3);
     double prob = (double)z32;
     prob += (double)w4[8].x * bias;
+#if SC_ABL_EXTRA_EXP  // timing ablation: one more f64 exp per item, result unused
+    if (exp(-prob * 1.0000001) == -1.0) prob = 0.0;
+#endif
     prob = 1.0 / (1.0 + exp(-prob));
     return (float)prob;
 }
@@ -166,11 +188,11 @@ __device__ __forceinline__ unsigned xcc_id() {
     return x & (kXcds - 1);
 }
 
-// LDS: weights [K][36] f32 | bias [K] f64 | order [K] i16 | per wave: st_s,
-// sums f32[SA], P f32[kItemBuf], st_p i16[SA], surv u16[SA]
-// (SA = strip_max rounded to 64)
+// LDS: weights [K][36] f32 | bias [K] f64 | order [K] i16 | per wave:
+// P f32[kItemBuf], st_s f32[SA], surv u32[SA], st_p i8[SA]
+// (SA = strip_max * band_rows rounded to 64)
 __host__ __device__ inline size_t wave_scratch_bytes(int SA) {
-    return (size_t)SA * 12 + (size_t)kItemBuf * 4;
+    return (size_t)SA * 9 + (size_t)kItemBuf * 4;
 }
 constexpr int kLdsWeights = SC_PPATH_GLOBAL_W ? 0 : 1;
 __host__ __device__ inline size_t model_lds_bytes(int K) {
@@ -191,24 +213,23 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
     }
     __syncthreads();  // the only workgroup barrier: model staged, waves now independent
 
-    const int SA = (a.strip_max + 63) & ~63;
+    const int SA = (a.strip_max * a.band_rows + 63) & ~63;
     unsigned char *ws = smem + model_lds_bytes(K) + (size_t)wv * wave_scratch_bytes(SA);
-    float *st_s = reinterpret_cast<float *>(ws);
-    float *sums = st_s + SA;
-    float *P = sums + SA;
-    int16_t *st_p = reinterpret_cast<int16_t *>(P + kItemBuf);
-    uint16_t *surv = reinterpret_cast<uint16_t *>(st_p + SA);
+    float *P = reinterpret_cast<float *>(ws);
+    float *st_s = P + kItemBuf;
+    unsigned *surv = reinterpret_cast<unsigned *>(st_s + SA);
+    int8_t *st_p = reinterpret_cast<int8_t *>(surv + SA);
 
     const TableGeom g = a.g;
-    const int half_off = g.step * g.Qp;
-    const int n_tasks = a.n_frames * a.n_rows * a.n_sub, nseg = kXcds * a.n_sub;
+    const int half_off = g.hs, cs = g.cs, row_cells = g.step * g.rowp;
+    const int n_tasks = a.n_frames * a.n_bands * a.n_sub, nseg = kXcds * a.n_sub;
     int q = (int)xcc_id(), empty = 0;
     // dequeue: one atomic per task on this XCD's queue word; the next task's
     // index and descriptor are fetched while the current task runs
     auto task_index = [&](int t) {  // queue position -> descriptor slot, frame
         const int rt = t / a.n_sub, sub = t - rt * a.n_sub;
-        const int frame = rt / a.n_rows, row = rt - frame * a.n_rows;
-        return make_int2(row * nseg + q * a.n_sub + sub, frame);
+        const int frame = rt / a.n_bands, band = rt - frame * a.n_bands;
+        return make_int2(band * nseg + q * a.n_sub + sub, frame);
     };
     int t = 0;
     if (lane == 0) t = atomicAdd(&a.queues[q * kQueueStride], 1);
@@ -235,7 +256,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
         int tn = 0;  // prefetch the next task index
         if (lane == 0) tn = atomicAdd(&a.queues[q * kQueueStride], 1);
         const int frame = tf.y;
-        const int nw = D.nw;
+        const int nw = D.nw, nr = D.nr;
         if (nw <= 0) {  // empty strip (narrow row)
             t = __builtin_amdgcn_readfirstlane(tn);
             if (t < n_tasks) {
@@ -244,25 +265,34 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
             }
             continue;
         }
-        // origin cell (phase 0, half 0) of window j0 of this row
+        // the frame's table; window (r, u) of the band has its origin cell
+        // (phase 0, half 0) at D.t_off + r*row_cells + u
+        const char *Tb = reinterpret_cast<const char *>(a.table + (long long)frame * g.frame4);
         const float4 *T = a.table + (long long)frame * g.frame4 + D.t_off;
+        // a survivor is (r << 16 | u); its LDS slot r*nw + u
+        auto cell = [&](unsigned sv) {
+            return (unsigned)D.t_off + (sv >> 16) * row_cells + (sv & 0xffffu) * cs;
+        };
+        auto slot = [&](unsigned sv) { return (int)(sv >> 16) * nw + (int)(sv & 0xffffu); };
 
-        // 1) prefilter; survivors (local window index u) in x order
+        // 1) prefilter; survivors in (row, x) order
         int nsurv = 0;
-        for (int b = 0; b < nw; b += 64) {
-            const int u = b + lane;
-            bool pass = false;
-            if (u < nw) {
-                const float4 *t0 = T + u;
-                const float4 v = box4(t0[0], t0[D.pre_row + D.pre_col], t0[D.pre_col], t0[D.pre_row]);
-                const float m = (((v.x + v.y) + v.z) + v.w) / 2.0f;  // sum(), :351-358
-                pass = m > D.thr;                                    // ObjDetector.cpp:188
-                st_p[u] = pass ? 0 : -1;
-                st_s[u] = 0.0f;
+        for (int r = 0; r < nr; r++) {
+            for (int b = 0; b < nw; b += 64) {
+                const int u = b + lane;
+                bool pass = false;
+                if (u < nw) {
+                    const float4 *t0 = T + r * row_cells + u * cs;
+                    const float4 v = box4(t0[0], t0[D.pre_row + D.pre_col], t0[D.pre_col], t0[D.pre_row]);
+                    const float m = (((v.x + v.y) + v.z) + v.w) / 2.0f;  // sum(), :351-358
+                    pass = m > D.thr;                                    // ObjDetector.cpp:188
+                    st_p[r * nw + u] = pass ? 0 : -1;
+                    st_s[r * nw + u] = 0.0f;
+                }
+                const unsigned long long mk = __ballot(pass);
+                if (pass) surv[nsurv + __popcll(mk & lanes_below())] = ((unsigned)r << 16) | (unsigned)u;
+                nsurv += __popcll(mk);
             }
-            const unsigned long long mk = __ballot(pass);
-            if (pass) surv[nsurv + __popcll(mk & lanes_below())] = (uint16_t)u;
-            nsurv += __popcll(mk);
         }
         wave_sync();
 
@@ -270,18 +300,41 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
         const ProjPatch *projL = a.proj + (long long)D.level * K;
         for (int s = 0; s < a.n_stages && nsurv > 0; s++) {
             const int off = a.stage_off[s], n = a.stage_off[s + 1] - off;
+            const float th = a.theta[s];
+            int nn = 0;
+            // stage decision of one survivor (GentleAdaboost.cpp:259;
+            // ObjDetector.cpp:197) and in-place order-preserving compaction:
+            // kept survivors move to [nn, ...), never past the group just read
+            auto decide = [&](bool valid, unsigned sv, float sum) {
+                bool keep = false;
+                if (valid) {
+                    const float sc = sum / (float)n;
+                    const int li = slot(sv);
+                    st_s[li] = sc;
+                    keep = !((double)sc < (double)th);
+                    st_p[li] = (int8_t)(keep ? s + 1 : s);
+                }
+                const unsigned long long mk = __ballot(keep);
+                wave_sync();
+                if (keep) surv[nn + __popcll(mk & lanes_below())] = sv;
+                nn += __popcll(mk);
+                wave_sync();
+            };
             if (nsurv >= a.chunk_min || n > kItemBuf) {
+                // one lane per survivor, k wave-uniform: parameters via scalar loads
                 for (int c = 0; c < nsurv; c += 64) {
                     const int i = c + lane;
+                    unsigned sv = 0;
+                    float sum = 0.0f;
                     if (i < nsurv) {
-                        const float4 *Tj = T + surv[i];
-                        float sum = 0.0f;
-                        for (int k = 0; k < n; k++) {  // k uniform: parameters via scalar loads
+                        sv = surv[i];
+                        const TabView Tj{Tb, cell(sv) << 4};
+                        for (int k = 0; k < n; k++) {
                             const int gk = off + k;
                             sum += weak_eval(Tj, half_off, projL[gk], a.w + gk * 9, a.bias[gk]);
                         }
-                        sums[i] = sum;
                     }
+                    decide(i < nsurv, sv, sum);
                 }
             } else {
                 // (survivor, weak) items over the lanes, groups of G survivors
@@ -298,51 +351,33 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
                         if (i < 0) { kk--; i += G; }
                         else if (i >= G) { kk++; i -= G; }
                         const int k = Ol[off + kk], gk = off + k;
+                        const TabView Tj{Tb, cell(surv[c + i]) << 4};
 #if SC_PPATH_GLOBAL_W
-                        P[k * G + i] = weak_eval(T + surv[c + i], half_off, projL[gk], a.w + gk * 9, a.bias[gk]);
+                        P[k * G + i] = weak_eval(Tj, half_off, projL[gk], a.w + gk * 9, a.bias[gk]);
 #else
-                        P[k * G + i] = weak_eval(T + surv[c + i], half_off, projL[gk], Wl + gk * 9, Bl[gk]);
+                        P[k * G + i] = weak_eval(Tj, half_off, projL[gk], Wl + gk * 9, Bl[gk]);
 #endif
                     }
                     wave_sync();
+                    unsigned sv = 0;
+                    float acc = 0.0f;  // GentleAdaboost.cpp:255-258 order
                     if (lane < G) {
-                        float acc = 0.0f;  // GentleAdaboost.cpp:255-258 order
+                        sv = surv[c + lane];
                         for (int k = 0; k < n; k++) acc += P[k * G + lane];
-                        sums[c + lane] = acc;
                     }
-                    wave_sync();
+                    decide(lane < G, sv, acc);
                 }
-            }
-            wave_sync();
-            // stage decision (GentleAdaboost.cpp:259; ObjDetector.cpp:197) and
-            // in-place order-preserving compaction
-            const float th = a.theta[s];
-            int nn = 0;
-            for (int b = 0; b < nsurv; b += 64) {
-                const int i = b + lane;
-                bool keep = false;
-                int u = 0;
-                if (i < nsurv) {
-                    u = surv[i];
-                    const float sc = sums[i] / (float)n;
-                    st_s[u] = sc;
-                    keep = !((double)sc < (double)th);
-                    st_p[u] = (int16_t)(keep ? s + 1 : s);
-                }
-                const unsigned long long mk = __ballot(keep);
-                wave_sync();
-                if (keep) surv[nn + __popcll(mk & lanes_below())] = (uint16_t)u;
-                nn += __popcll(mk);
             }
             nsurv = nn;
-            wave_sync();
         }
 
-        // 3) per-window results to HBM (coalesced)
+        // 3) per-window results to HBM (coalesced per row)
         const long long gi = (long long)frame * a.grid_per_frame + D.g_off;
-        for (int u = lane; u < nw; u += 64) {
-            a.st_p[gi + u] = (int8_t)st_p[u];
-            a.st_s[gi + u] = st_s[u];
+        for (int r = 0; r < nr; r++) {
+            for (int u = lane; u < nw; u += 64) {
+                a.st_p[gi + (long long)r * D.g_row + u] = st_p[r * nw + u];
+                a.st_s[gi + (long long)r * D.g_row + u] = st_s[r * nw + u];
+            }
         }
         wave_sync();
         t = __builtin_amdgcn_readfirstlane(tn);
@@ -445,7 +480,7 @@ __global__ __launch_bounds__(64) void walk_kernel(WalkArgs a) {
 }  // namespace
 
 int launch_cascade(const CascadeArgs &a, int device, hipStream_t s) {
-    const int SA = (a.strip_max + 63) & ~63;
+    const int SA = (a.strip_max * a.band_rows + 63) & ~63;
     const size_t lds = model_lds_bytes(a.K) + kWavesPerWg * wave_scratch_bytes(SA);
     static int cus = 0, dev_cached = -1;
     if (dev_cached != device) {
@@ -466,8 +501,8 @@ void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s) {
     hipLaunchKernelGGL(walk_kernel, dim3(a.n_rows * n_frames), dim3(64), 0, s, a);
 }
 
-size_t cascade_lds_bytes(int K, int strip_max) {
-    return model_lds_bytes(K) + kWavesPerWg * wave_scratch_bytes((strip_max + 63) & ~63);
+size_t cascade_lds_bytes(int K, int strip_max, int band_rows) {
+    return model_lds_bytes(K) + kWavesPerWg * wave_scratch_bytes((strip_max * band_rows + 63) & ~63);
 }
 
 }  // namespace sc

@@ -29,9 +29,11 @@ def _det_set(arr):
                    int(r["stage"]), float(r["score"])) for r in arr)
 
 
+@pytest.mark.parametrize("layout", ["0", "1"])
 @pytest.mark.parametrize("W,H,seed", [(640, 480, 1), (1920, 1080, 1000), (257, 131, 7), (2, 2, 3),
                                       (3000, 67, 5)])
-def test_integral_bit_exact(sc, oracle, W, H, seed):
+def test_integral_bit_exact(sc, oracle, monkeypatch, W, H, seed, layout):
+    monkeypatch.setenv("SC_TABLE_LAYOUT", layout)
     img = _frame(W, H, seed)
     det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1))
     det.detect(img)  # frames smaller than the window: no rows, integral still built
@@ -77,18 +79,26 @@ def test_grid_parity_default_levels_odd_size(sc, oracle, face_cascade):
     _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(), oracle.Params())
 
 
-@pytest.mark.parametrize("chunk_min,substrips", [("1", None), ("40", None), (None, "3")])
-def test_grid_parity_kernel_paths(sc, oracle, face_cascade, monkeypatch, chunk_min, substrips):
+@pytest.mark.parametrize("chunk_min,substrips,band_rows,layout", [
+    ("1", None, None, None), ("40", None, "3", "0"), (None, "3", "1", "1"), (None, "2", "5", None),
+    ("1", None, "2", "1"), (None, None, None, "0"), (None, None, None, "1")])
+def test_grid_parity_kernel_paths(sc, oracle, face_cascade, monkeypatch, chunk_min, substrips,
+                                  band_rows, layout):
     """The one-lane-per-window stage path (used for stages with more weak
-    classifiers than the item buffer holds) and other strip splits give the
-    same bits as the default item path."""
-    if chunk_min:
-        monkeypatch.setenv("SC_CHUNK_MIN", chunk_min)
-    if substrips:
-        monkeypatch.setenv("SC_SUBSTRIPS", substrips)
+    classifiers than the item buffer holds), other strip splits, band heights
+    and both table cell formats give the same bits as the defaults."""
+    for k, v in (("SC_CHUNK_MIN", chunk_min), ("SC_SUBSTRIPS", substrips),
+                 ("SC_BAND_ROWS", band_rows), ("SC_TABLE_LAYOUT", layout)):
+        if v:
+            monkeypatch.setenv(k, v)
     img = _frame(1280, 720, 77)
     _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=8),
                  oracle.Params(n_levels=8))
+    if layout:
+        det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1))
+        det.detect(img)
+        T = det.dump_integral(*img.shape[::-1])
+        assert T.view(np.uint32).tobytes() == oracle.integral(img).view(np.uint32).tobytes()
 
 
 def test_pedestrian_64x128(sc, oracle, ped_cascade):
