@@ -132,6 +132,23 @@ __device__ __forceinline__ void patch_features(const TabView &T, const ProjPatch
     }
 }
 
+// A ProjPatch as two 16-B loads issued together (the compiler would
+// otherwise fetch col[] only after branching on shape: a second round trip).
+__device__ __forceinline__ ProjPatch load_proj(const ProjPatch *p) {
+    const int4 *q = reinterpret_cast<const int4 *>(p);
+    const int4 a = q[0], b = q[1];
+    ProjPatch r;
+    r.shape = a.x;
+    r.row0 = a.y;
+    r.rowstep = a.z;
+    r.col[0] = a.w;
+    r.col[1] = b.x;
+    r.col[2] = b.y;
+    r.col[3] = b.z;
+    r.col[4] = b.w;
+    return r;
+}
+
 // One (window, weak classifier) item: CalcFeature + Normalize + Predict.
 // T views the window's origin cell (half 0); w4 = w[0..35] (LDS).
 __device__ __forceinline__ float weak_eval(const TabView &T, int half_off,
@@ -346,16 +363,23 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
                 for (int c = 0; c < nsurv; c += gcap) {
                     const int G = min(gcap, nsurv - c), items = G * n;
                     const float rcp = 1.0f / (float)G;
-                    for (int t2 = lane; t2 < items; t2 += 64) {
-                        int kk = (int)((float)t2 * rcp), i = t2 - kk * G;  // kk = t2 / G
+                    auto decode = [&](int t2, int &k, int &i) {  // item -> (weak k, survivor i)
+                        int kk = (int)((float)t2 * rcp);                // kk = t2 / G
+                        i = t2 - kk * G;
                         if (i < 0) { kk--; i += G; }
                         else if (i >= G) { kk++; i -= G; }
-                        const int k = Ol[off + kk], gk = off + k;
+                        k = Ol[off + kk];
+                    };
+                    for (int t2 = lane; t2 < items; t2 += 64) {
+                        int k, i;
+                        decode(t2, k, i);
+                        const int gk = off + k;
                         const TabView Tj{Tb, cell(surv[c + i]) << 4};
+                        const ProjPatch pj = load_proj(projL + gk);
 #if SC_PPATH_GLOBAL_W
-                        P[k * G + i] = weak_eval(Tj, half_off, projL[gk], a.w + gk * 9, a.bias[gk]);
+                        P[k * G + i] = weak_eval(Tj, half_off, pj, a.w + gk * 9, a.bias[gk]);
 #else
-                        P[k * G + i] = weak_eval(Tj, half_off, projL[gk], Wl + gk * 9, Bl[gk]);
+                        P[k * G + i] = weak_eval(Tj, half_off, pj, Wl + gk * 9, Bl[gk]);
 #endif
                     }
                     wave_sync();
