@@ -1,5 +1,7 @@
 """Benchmark: detection windows/s on the 1080p 24-level pyramid (BASELINE.json
-metric, config C2 on one GPU; C3-style frame sharding for --gpus N).
+metric, config C2 on one GPU; C3-style frame sharding for --gpus N).  --config
+C4 (4K, 32 levels) and C5 (64x128 pedestrian cascade) measure the other
+single-GPU configs the same way.
 
 A step = one pass of the detect path over one batch of synthetic 1080p frames
 already resident in HBM: gradient+integral (rowscan, colscan), prefilter +
@@ -7,7 +9,7 @@ cascade + adaptive-stride walk (windows), and the gather of the raw detection
 records (RCCL all_gather when N > 1).  value = stride-3 grid windows of all
 frames of all ranks / max-over-ranks wall time.  Prints one JSON line (rank 0).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C4|C5] [--batch B]
 """
 from __future__ import annotations
 
@@ -25,28 +27,63 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+MODELS = os.path.join(ROOT, "surfcascade_amd", "models")
+# BASELINE.json configs measured on one GPU (C1 is the CPU-only plumbing case;
+# C3 = C2 frame-sharded over --gpus N)
+CONFIGS = {
+    "C2": dict(width=1920, height=1080, levels=24, batch=16, model="face40_synth.cfg",
+               pedestrian=False,
+               metric="detection windows/sec on 1080p 24-scale pyramid",
+               desc="C2: %dx%d frames, %d-level window pyramid (l=70..%d), 40x40 face cascade "
+                    "10 stages / 190 weak LR"),
+    "C4": dict(width=3840, height=2160, levels=32, batch=4, model="face40_synth.cfg",
+               pedestrian=False,
+               metric="detection windows/sec on 4K 32-scale pyramid",
+               desc="C4: %dx%d frames, %d-level window pyramid (l=70..%d), 40x40 face cascade "
+                    "10 stages / 190 weak LR"),
+    "C5": dict(width=1920, height=1080, levels=23, batch=16, model="ped64x128_synth.cfg",
+               pedestrian=True,
+               metric="detection windows/sec, 64x128 pedestrian cascade on 1080p 23-scale pyramid",
+               desc="C5: %dx%d frames, %d-level window pyramid (l=64..%d, h=2l), 64x128 pedestrian "
+                    "cascade 10 stages / 380 weak LR"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16, help="1080p frames per GPU per step")
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--levels", type=int, default=24)
-    ap.add_argument("--model", default=os.path.join(ROOT, "surfcascade_amd", "models", "face40_synth.cfg"))
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, help="frames per GPU per step (config default)")
+    ap.add_argument("--width", type=int)
+    ap.add_argument("--height", type=int)
+    ap.add_argument("--levels", type=int)
+    ap.add_argument("--model")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
-    return ap.parse_args()
+    a = ap.parse_args()
+    c = CONFIGS[a.config]
+    for k in ("batch", "width", "height", "levels"):
+        if getattr(a, k) is None:
+            setattr(a, k, c[k])
+    if a.model is None:
+        a.model = os.path.join(MODELS, c["model"])
+    a.pedestrian = c["pedestrian"]
+    return a
 
 
-def cpu_baseline(frames, model_path, levels, seconds):
+def cpu_baseline(frames, model_path, levels, seconds, pedestrian=False):
     """The CPU restatement (oracle/, OpenMP over levels like ObjDetector.cpp:177)
     on a bounded sample of the same frames: in-memory u8 frame -> raw detections."""
     from oracle import oracle as O
     O.build()
-    casc = O.cascade_from_cfg(open(model_path).read())
-    params = O.Params(n_levels=levels)
+    if pedestrian:
+        casc = O.cascade_from_cfg(open(model_path).read(), tmpl_w=64, tmpl_h=128)
+        params = O.Params(base_len=64, aspect_h=2, n_levels=levels)
+    else:
+        casc = O.cascade_from_cfg(open(model_path).read())
+        params = O.Params(n_levels=levels)
     H, W = frames.shape[1:]
     grid = O.grid_count(W, H, params)
     try:
@@ -98,7 +135,8 @@ def main():
     start, _ = shard_range(B * world, world, rank)
     host_frames = synth.make_frames(W, H, B, seed0=1000 + start)
     frames = torch.from_numpy(host_frames).to(f"cuda:{local_rank}")
-    params = sc.ScanParams(n_levels=args.levels)
+    params = (sc.ScanParams.pedestrian(n_levels=args.levels) if args.pedestrian
+              else sc.ScanParams(n_levels=args.levels))
     det = sc.Detector(args.model, params, device=local_rank)
     cap = 256 * B
     recs = torch.zeros(cap * sc.RECORD_DTYPE.itemsize, dtype=torch.uint8, device=frames.device)
@@ -155,10 +193,11 @@ def main():
         if os.path.exists(pmc_path):
             with open(pmc_path) as f:
                 pm = json.load(f)
-            if pm.get("batch") == B and pm.get("width") == W and pm.get("levels") == args.levels:
+            if (pm.get("batch") == B and pm.get("width") == W and pm.get("levels") == args.levels
+                    and pm.get("config", "C2") == args.config):
                 traffic = pm.get("hbm_bytes_per_launch")
         line = {
-            "metric": "detection windows/sec on 1080p 24-scale pyramid",
+            "metric": CONFIGS[args.config]["metric"],
             "value": value,
             "unit": "windows/s",
             "n_gpus": world,
@@ -169,17 +208,17 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded 1080p frames, seeded 10-stage 40x40 cascade, thetas calibrated "
-                    "on held-out frames)",
-            "config": {"workload": "C2: %dx%d frames, %d-level window pyramid (l=70..%d), 40x40 face "
-                                   "cascade 10 stages / 190 weak LR; frame-sharded, %d frames per GPU "
-                                   "per step" % (W, H, args.levels,
-                                                  int(70 * 1.1 ** (args.levels - 1)), B),
+            "data": "synthetic (seeded %dx%d frames, seeded 10-stage %s cascade, thetas calibrated "
+                    "on held-out frames)" % (W, H, "64x128" if args.pedestrian else "40x40"),
+            "config": {"workload": (CONFIGS[args.config]["desc"] + "; frame-sharded, %d frames per "
+                                    "GPU per step") % (W, H, args.levels,
+                                                       params.level_len(args.levels - 1), B),
+                       "name": args.config,
                        "frames_per_gpu_per_step": B, "grid_windows_per_frame": grid,
                        "levels": args.levels, "parallelism": "frame-sharded dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "window_kernel", "avg_launch_ms": avg_win_s * 1e3,
+                         "kernel": "cascade_kernel", "avg_launch_ms": avg_win_s * 1e3,
                          "bytes_per_launch": tab_bytes * B,
                          "pipeline_achieved": pipe_bytes * B / pipe_s / 1e9,
                          "pipeline_frac": pipe_bytes * B / pipe_s / 1e9 / HBM_PEAK_GBS},
@@ -188,7 +227,8 @@ def main():
             "detections_last_step": total_det,
         }
         if not args.no_cpu and world == 1:
-            line["cpu_baseline"] = cpu_baseline(host_frames, args.model, args.levels, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(host_frames, args.model, args.levels, args.cpu_seconds,
+                                                args.pedestrian)
             line["vs_cpu"] = value / world / line["cpu_baseline"]["value"]
         print(json.dumps(line), flush=True)
     if dist is not None:

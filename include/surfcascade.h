@@ -144,6 +144,33 @@ int sc_set_timing(sc_detector *d, int on);
 int sc_get_timing(sc_detector *d, double ms_total[SC_KERNEL_COUNT],
                   int64_t launches[SC_KERNEL_COUNT]);
 
+/* ---- post-processing (ObjDetector.cpp:223-231) --------------------------
+ * cv::groupRectangles(wins, weights = 0s, levelWeights = scores, 2, 0.2)
+ * (OpenCV 3.0.0 objdetect, called at ObjDetector.cpp:224-225) and the FDDB
+ * text block the reference writes per image (:228-231). */
+typedef struct {
+    int32_t x, y, width, height; /* cv::Rect                                 */
+    double score;                /* levelWeight: the cluster's best score    */
+} sc_scored_rect;
+
+/* Cluster rectangles (SimilarRects(eps) components), keep clusters with more
+ * than group_threshold members that are not inside a better-supported one;
+ * each output is the members' mean rectangle with their maximum score.
+ * *n_out = output count (SC_ERR_CAPACITY when it exceeds capacity). */
+int sc_group_rectangles(const sc_scored_rect *in, int n, int group_threshold,
+                        double eps, sc_scored_rect *out, int capacity,
+                        int *n_out);
+/* The same per frame over raw detection records of n_frames frames (any
+ * order; each frame's rectangles enter in canonical (level, y, x) order).
+ * Frames' results back to back in out; frame_counts[f] = frame f's count. */
+int sc_group_detections(const sc_det_record *rec, int n, int n_frames,
+                        int group_threshold, double eps, sc_scored_rect *out,
+                        int capacity, int32_t *frame_counts, int *n_out);
+/* "name\ncount\nx y w h score\n..." (std::ostream default double format).
+ * *len = bytes needed (excluding NUL); SC_ERR_CAPACITY if cap <= *len. */
+int sc_fddb_format(const char *image_name, const sc_scored_rect *r, int n,
+                   char *buf, size_t cap, size_t *len);
+
 const char *sc_last_error(void);
 const char *sc_version(void);
 

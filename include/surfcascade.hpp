@@ -124,6 +124,45 @@ inline std::vector<Rect> ExtractPatches(int tmpl_w = 40, int tmpl_h = 40) {
     return out;
 }
 
+// cv::groupRectangles(rectList, weights, levelWeights, groupThreshold, eps)
+// as ObjDetector.cpp:224-225 calls it (weights all 0, levelWeights = scores):
+// rectList becomes the cluster means, levelWeights their best scores and
+// weights 0 per output rectangle.
+inline void groupRectangles(std::vector<Rect> &rectList, std::vector<int> &weights,
+                            std::vector<double> &levelWeights, int groupThreshold,
+                            double eps = 0.2) {
+    if (levelWeights.size() != rectList.size()) throw Error(SC_ERR_INVALID, "levelWeights size");
+    std::vector<sc_scored_rect> in(rectList.size()), out(rectList.size() + 1);
+    for (size_t i = 0; i < rectList.size(); i++)
+        in[i] = {rectList[i].x, rectList[i].y, rectList[i].width, rectList[i].height,
+                 levelWeights[i]};
+    int n = 0;
+    check(sc_group_rectangles(in.data(), (int)in.size(), groupThreshold, eps, out.data(),
+                              (int)out.size(), &n));
+    rectList.clear();
+    levelWeights.clear();
+    for (int i = 0; i < n; i++) {
+        rectList.push_back({out[i].x, out[i].y, out[i].width, out[i].height});
+        levelWeights.push_back(out[i].score);
+    }
+    weights.assign(n, 0);
+}
+
+// The per-image block of the reference's output file (ObjDetector.cpp:228-231).
+inline std::string FddbBlock(const std::string &name, const std::vector<Rect> &wins,
+                             const std::vector<double> &scores) {
+    std::vector<sc_scored_rect> r(wins.size());
+    for (size_t i = 0; i < wins.size(); i++)
+        r[i] = {wins[i].x, wins[i].y, wins[i].width, wins[i].height, scores[i]};
+    size_t len = 0;
+    int rc = sc_fddb_format(name.c_str(), r.data(), (int)r.size(), nullptr, 0, &len);
+    if (rc != SC_ERR_CAPACITY) check(rc);
+    std::string s(len + 1, '\0');
+    check(sc_fddb_format(name.c_str(), r.data(), (int)r.size(), &s[0], s.size(), &len));
+    s.resize(len);
+    return s;
+}
+
 inline sc_scan_params DefaultScanParams() {
     sc_scan_params p;
     sc_scan_params_default(&p);

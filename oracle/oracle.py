@@ -91,12 +91,39 @@ def lib():
                                        ctypes.POINTER(ScoModel), ctypes.POINTER(ScoParams),
                                        ctypes.c_void_p, ctypes.c_int64, _i64p, ctypes.c_int, _f32p]
         L.sco_detect_frame.restype = ctypes.c_int64
+        L.sco_group_rectangles.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_double, ctypes.c_void_p]
+        L.sco_fddb_format.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int,
+                                      ctypes.c_char_p, ctypes.c_long]
+        L.sco_fddb_format.restype = ctypes.c_long
         _lib = L
     return _lib
 
 
 def _p(a, t):
     return a.ctypes.data_as(t)
+
+
+RECT_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("width", "<i4"), ("height", "<i4"),
+                       ("score", "<f8")])
+
+
+def group_rectangles(rects, group_threshold=2, eps=0.2):
+    """cv::groupRectangles restated (sc_oracle_group.c); rects: RECT_DTYPE."""
+    r = np.ascontiguousarray(rects, RECT_DTYPE)
+    out = np.zeros(max(len(r), 1), RECT_DTYPE)
+    n = lib().sco_group_rectangles(r.ctypes.data if len(r) else None, len(r), group_threshold,
+                                   eps, out.ctypes.data)
+    return out[:n].copy()
+
+
+def fddb_format(name, rects):
+    r = np.ascontiguousarray(rects, RECT_DTYPE)
+    data = r.ctypes.data if len(r) else None
+    need = lib().sco_fddb_format(name.encode(), data, len(r), None, 0)
+    buf = ctypes.create_string_buffer(need + 1)
+    lib().sco_fddb_format(name.encode(), data, len(r), buf, need + 1)
+    return buf.value.decode()
 
 
 # --------------------------------------------------------------------------

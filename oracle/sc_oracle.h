@@ -92,6 +92,16 @@ int64_t sco_detect_frame(const uint8_t *img, int W, int H, int stride,
                          sco_window *out, int64_t cap, int64_t *n_visited,
                          int nthreads, float *scratch_T);
 
+/* Post-processing (sc_oracle_group.c): groupRectangles + FDDB block. */
+typedef struct {
+    int32_t x, y, w, h;
+    double score;
+} sco_rect;
+
+int sco_group_rectangles(const sco_rect *in, int n, int group_threshold, double eps,
+                         sco_rect *out);
+long sco_fddb_format(const char *name, const sco_rect *r, int n, char *buf, long cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -19,7 +19,8 @@ import numpy as np
 
 __all__ = ["ScanParams", "Model", "CascadeClassifier", "StageClassifier", "LogisticRegression",
            "Detector", "SurfCascadeError", "WINDOW_DTYPE", "RECORD_DTYPE", "library_path",
-           "load_library", "extract_patches"]
+           "load_library", "extract_patches", "RECT_DTYPE", "groupRectangles", "group_detections",
+           "fddb_format"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -35,6 +36,9 @@ RECORD_DTYPE = np.dtype([("frame", "<i4"), ("level", "<i4"), ("x", "<i4"), ("y",
                          ("w", "<i4"), ("h", "<i4"), ("stage", "<i4"), ("pad", "<i4"),
                          ("score", "<f8")])
 
+RECT_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("width", "<i4"), ("height", "<i4"),
+                       ("score", "<f8")])
+
 KERNELS = ("rowscan", "colscan", "windows", "walk")
 
 # every symbol include/surfcascade.h declares
@@ -44,6 +48,7 @@ EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_mode
            "sc_detector_destroy", "sc_detect", "sc_detect_batch", "sc_detect_device",
            "sc_enqueue_device", "sc_synchronize", "sc_detector_stream", "sc_detector_info",
            "sc_detector_set_debug", "sc_debug_dump", "sc_set_timing", "sc_get_timing",
+           "sc_group_rectangles", "sc_group_detections", "sc_fddb_format",
            "sc_last_error", "sc_version")
 
 
@@ -67,6 +72,10 @@ class ScanParams(ctypes.Structure):
         d.update(kw)
         for k, v in d.items():
             setattr(self, k, v)
+
+    def level_len(self, i):
+        """Window side of level i: (int)(base_len * scale_factor^i) (ObjDetector.cpp:180)."""
+        return int(self.base_len * self.scale_factor ** i)
 
     @classmethod
     def pedestrian(cls, **kw):
@@ -130,6 +139,9 @@ def load_library():
     L.sc_debug_dump.argtypes = [vp, i32, i32, vp, sz]
     L.sc_set_timing.argtypes = [vp, i32]
     L.sc_get_timing.argtypes = [vp, P(ctypes.c_double), P(i64)]
+    L.sc_group_rectangles.argtypes = [vp, i32, i32, ctypes.c_double, vp, i32, P(i32)]
+    L.sc_group_detections.argtypes = [vp, i32, i32, i32, ctypes.c_double, vp, i32, vp, P(i32)]
+    L.sc_fddb_format.argtypes = [ctypes.c_char_p, vp, i32, ctypes.c_char_p, sz, P(sz)]
     _lib = L
     return L
 
@@ -147,6 +159,62 @@ def extract_patches(tmpl_w=40, tmpl_h=40):
     r = np.zeros((n, 4), np.int32)
     L.sc_extract_patches(tmpl_w, tmpl_h, r.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n)
     return r
+
+
+# ---------------------------------------------------------------------------
+# post-processing (ObjDetector.cpp:223-231)
+# ---------------------------------------------------------------------------
+
+def _as_rects(rects):
+    """RECT_DTYPE array from a RECT_DTYPE / WINDOW_DTYPE / RECORD_DTYPE array."""
+    a = np.asarray(rects)
+    if a.dtype == RECT_DTYPE:
+        return np.ascontiguousarray(a)
+    r = np.zeros(len(a), RECT_DTYPE)
+    r["x"], r["y"], r["score"] = a["x"], a["y"], a["score"]
+    r["width"], r["height"] = a["w"], a["h"]
+    return r
+
+
+def groupRectangles(rects, groupThreshold=2, eps=0.2):
+    """cv::groupRectangles(wins, weights = 0s, levelWeights = scores, 2, 0.2) as the
+    reference calls it (ObjDetector.cpp:224-225): mean rectangle and best score of
+    each SimilarRects cluster with more than groupThreshold members."""
+    L = load_library()
+    r = _as_rects(rects)
+    out = np.zeros(max(len(r), 1), RECT_DTYPE)
+    n = ctypes.c_int32(0)
+    _check(L.sc_group_rectangles(r.ctypes.data if len(r) else None, len(r), int(groupThreshold),
+                                 float(eps), out.ctypes.data, len(out), ctypes.byref(n)))
+    return out[:n.value].copy()
+
+
+def group_detections(records, n_frames, groupThreshold=2, eps=0.2):
+    """groupRectangles per frame over RECORD_DTYPE detections -> list of RECT_DTYPE arrays."""
+    L = load_library()
+    rec = np.ascontiguousarray(records, RECORD_DTYPE)
+    out = np.zeros(max(len(rec), 1), RECT_DTYPE)
+    counts = np.zeros(max(n_frames, 1), np.int32)
+    n = ctypes.c_int32(0)
+    _check(L.sc_group_detections(rec.ctypes.data if len(rec) else None, len(rec), n_frames,
+                                 int(groupThreshold), float(eps), out.ctypes.data, len(out),
+                                 counts.ctypes.data, ctypes.byref(n)))
+    offs = np.concatenate([[0], np.cumsum(counts[:n_frames])])
+    return [out[offs[f]:offs[f + 1]].copy() for f in range(n_frames)]
+
+
+def fddb_format(name, rects):
+    """The per-image block of the reference's surf.txt (ObjDetector.cpp:228-231)."""
+    L = load_library()
+    r = _as_rects(rects)
+    need = ctypes.c_size_t(0)
+    data = r.ctypes.data if len(r) else None
+    rc = L.sc_fddb_format(name.encode(), data, len(r), None, 0, ctypes.byref(need))
+    if rc < 0 and rc != -6:
+        _check(rc)
+    buf = ctypes.create_string_buffer(need.value + 1)
+    _check(L.sc_fddb_format(name.encode(), data, len(r), buf, need.value + 1, ctypes.byref(need)))
+    return buf.value.decode()
 
 
 # ---------------------------------------------------------------------------

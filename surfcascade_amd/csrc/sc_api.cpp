@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "sc_kernels.hpp"
+#include "sc_group.hpp"
 #include "sc_model.hpp"
 #include "surfcascade.h"
 
@@ -646,6 +647,71 @@ int sc_model_weak(const sc_model *m, int s, int k, int *patch_index, float w33[3
 }
 
 void sc_model_free(sc_model *m) { delete m; }
+
+int sc_group_rectangles(const sc_scored_rect *in, int n, int group_threshold, double eps,
+                        sc_scored_rect *out, int capacity, int *n_out) {
+    return guarded([&] {
+        if ((n > 0 && !in) || n < 0 || !n_out) throw Error{SC_ERR_INVALID, "null argument"};
+        const std::vector<sc_scored_rect> g = sc::group_rectangles(in, n, group_threshold, eps);
+        *n_out = (int)g.size();
+        if (out) std::copy(g.begin(), g.begin() + std::min<size_t>(g.size(), std::max(capacity, 0)), out);
+        if ((int)g.size() > capacity) throw Error{SC_ERR_CAPACITY, "output capacity too small"};
+        return SC_OK;
+    });
+}
+
+int sc_group_detections(const sc_det_record *rec, int n, int n_frames, int group_threshold,
+                        double eps, sc_scored_rect *out, int capacity, int32_t *frame_counts,
+                        int *n_out) {
+    return guarded([&] {
+        if ((n > 0 && !rec) || n < 0 || n_frames < 0 || !n_out || (n_frames > 0 && !frame_counts))
+            throw Error{SC_ERR_INVALID, "null argument"};
+        std::vector<int> idx(n);
+        for (int i = 0; i < n; i++) {
+            if (rec[i].frame < 0 || rec[i].frame >= n_frames)
+                throw Error{SC_ERR_INVALID, "record frame index out of range"};
+            idx[i] = i;
+        }
+        std::sort(idx.begin(), idx.end(), [&](int a, int b) {
+            const sc_det_record &p = rec[a], &q = rec[b];
+            if (p.frame != q.frame) return p.frame < q.frame;
+            if (p.level != q.level) return p.level < q.level;
+            if (p.y != q.y) return p.y < q.y;
+            return p.x < q.x;
+        });
+        int total = 0;
+        std::vector<sc_scored_rect> rects;
+        for (int f = 0, i = 0; f < n_frames; f++) {
+            rects.clear();
+            for (; i < n && rec[idx[i]].frame == f; i++) {
+                const sc_det_record &r = rec[idx[i]];
+                rects.push_back(sc_scored_rect{r.x, r.y, r.w, r.h, r.score});
+            }
+            const std::vector<sc_scored_rect> g =
+                sc::group_rectangles(rects.data(), (int)rects.size(), group_threshold, eps);
+            frame_counts[f] = (int)g.size();
+            for (const sc_scored_rect &r : g) {
+                if (out && total < capacity) out[total] = r;
+                total++;
+            }
+        }
+        *n_out = total;
+        if (total > capacity) throw Error{SC_ERR_CAPACITY, "output capacity too small"};
+        return SC_OK;
+    });
+}
+
+int sc_fddb_format(const char *name, const sc_scored_rect *r, int n, char *buf, size_t cap,
+                   size_t *len) {
+    return guarded([&] {
+        if (!name || (n > 0 && !r) || n < 0 || !len) throw Error{SC_ERR_INVALID, "null argument"};
+        const std::string s = sc::fddb_block(name, r, n);
+        *len = s.size();
+        if (!buf || cap <= s.size()) throw Error{SC_ERR_CAPACITY, "buffer too small"};
+        std::memcpy(buf, s.c_str(), s.size() + 1);
+        return SC_OK;
+    });
+}
 
 int sc_extract_patches(int tw, int th, int32_t *rects, int cap) {
     if (tw < 1 || th < 1) return fail(SC_ERR_INVALID, "bad template size");

@@ -40,6 +40,9 @@ int main(int argc, char **argv) {
         for (size_t i = 0; i < wins.size(); i++)
             std::printf("%d %d %d %d %.17g\n", wins[i].x, wins[i].y, wins[i].width, wins[i].height,
                         scores[i]);
+        std::vector<int> weights(wins.size(), 0);  // ObjDetector.cpp:223-225
+        surfcascade::groupRectangles(wins, weights, scores, 2, 0.2);
+        std::printf("%s", surfcascade::FddbBlock("frame", wins, scores).c_str());
     }
     return 0;
 }

@@ -46,8 +46,13 @@ def test_facade_detect_matches_oracle(facade_bin, tmp_path, oracle):
     assert r.returncode == 0, r.stderr
     lines = r.stdout.splitlines()
     k = [i for i, l in enumerate(lines) if l.startswith("detections")][0]
-    got = [tuple(l.split()) for l in lines[k + 1:]]
+    nd = int(lines[k].split()[1])
+    got = [tuple(l.split()) for l in lines[k + 1:k + 1 + nd]]
     ref, _ = oracle.detect(oracle.integral(img), c, oracle.Params(n_levels=3))
     exp = [(str(d["x"]), str(d["y"]), str(d["w"]), str(d["h"]), "%.17g" % d["score"]) for d in ref]
-    assert int(lines[k].split()[1]) == len(ref)
+    assert nd == len(ref)
     assert got == exp
+    # then groupRectangles + the FDDB block (ObjDetector.cpp:223-231)
+    import surfcascade_amd as sc
+    block = "\n".join(lines[k + 1 + nd:]) + "\n"
+    assert block == oracle.fddb_format("frame", oracle.group_rectangles(sc._as_rects(ref)))

@@ -174,3 +174,26 @@ def test_capacity_error_reports_count(sc):
     with pytest.raises(sc.SurfCascadeError) as e:
         det.detect(img, capacity=3)
     assert e.value.code == -6
+
+
+def test_grouped_detections_match_oracle(sc, oracle, face_cascade):
+    """Detect (GPU) -> groupRectangles (host) equals the oracle's detect -> group,
+    i.e. the reference's surf.txt block for the frame (ObjDetector.cpp:224-231)."""
+    from surfcascade_amd import synth
+    c = face_cascade
+    theta = np.full(c.n_stages, 0.25, np.float32)
+    text = synth.write_cfg(synth.cascade_tree(c.n_weak, theta, c.patch_index, c.w, c.bias))
+    det = sc.Detector(sc.Model.parse(text), sc.ScanParams(n_levels=6))
+    frames = np.stack([_frame(640, 480, 500 + k) for k in range(3)])
+    got = det.detect_batch(frames)
+    casc_or = oracle.cascade_from_cfg(text)
+    n_groups = 0
+    for k in range(3):
+        ref, _ = oracle.detect(oracle.integral(frames[k]), casc_or, oracle.Params(n_levels=6))
+        assert _det_set(got[k]) == _det_set(ref)
+        a = sc.groupRectangles(got[k])
+        b = oracle.group_rectangles(sc._as_rects(ref))
+        assert a.tobytes() == b.tobytes()
+        assert sc.fddb_format("f%d" % k, a) == oracle.fddb_format("f%d" % k, b)
+        n_groups += len(a)
+    assert n_groups > 0
