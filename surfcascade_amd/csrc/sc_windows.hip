@@ -38,9 +38,6 @@ namespace sc {
 
 namespace {
 
-#ifndef SC_PPATH_GLOBAL_W
-#define SC_PPATH_GLOBAL_W 0
-#endif
 #ifndef SC_CASCADE_MIN_WGS  // workgroups per CU the register budget must allow
 #define SC_CASCADE_MIN_WGS 1
 #endif
@@ -211,27 +208,30 @@ __device__ __forceinline__ unsigned xcc_id() {
 __host__ __device__ inline size_t wave_scratch_bytes(int SA) {
     return (size_t)SA * 9 + (size_t)kItemBuf * 4;
 }
-constexpr int kLdsWeights = SC_PPATH_GLOBAL_W ? 0 : 1;
-__host__ __device__ inline size_t model_lds_bytes(int K) {
-    return kLdsWeights * ((size_t)K * 144 + (size_t)K * 8) + (((size_t)K * 2 + 15) & ~(size_t)15);
+// LW: weights and biases staged in LDS (else read through the caches: models
+// whose weights do not fit the LDS)
+__host__ __device__ inline size_t model_lds_bytes(int K, bool LW) {
+    return (LW ? (size_t)K * 144 + (size_t)K * 8 : 0) + (((size_t)K * 2 + 15) & ~(size_t)15);
 }
 
+template <bool LW>
 __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_kernel(CascadeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int K = a.K;
     float4 *Wl = reinterpret_cast<float4 *>(smem);
-    double *Bl = reinterpret_cast<double *>(smem + kLdsWeights * (size_t)K * 144);
-    int16_t *Ol = reinterpret_cast<int16_t *>(Bl + kLdsWeights * K);
-    for (int i = tid; i < kLdsWeights * K * 9; i += kCascadeThreads) Wl[i] = a.w[i];
+    double *Bl = reinterpret_cast<double *>(smem + (LW ? (size_t)K * 144 : 0));
+    int16_t *Ol = reinterpret_cast<int16_t *>(Bl + (LW ? K : 0));
+    if (LW)
+        for (int i = tid; i < K * 9; i += kCascadeThreads) Wl[i] = a.w[i];
     for (int i = tid; i < K; i += kCascadeThreads) {
-        if (kLdsWeights) Bl[i] = a.bias[i];
+        if (LW) Bl[i] = a.bias[i];
         Ol[i] = a.order[i];
     }
     __syncthreads();  // the only workgroup barrier: model staged, waves now independent
 
     const int SA = (a.strip_max * a.band_rows + 63) & ~63;
-    unsigned char *ws = smem + model_lds_bytes(K) + (size_t)wv * wave_scratch_bytes(SA);
+    unsigned char *ws = smem + model_lds_bytes(K, LW) + (size_t)wv * wave_scratch_bytes(SA);
     float *P = reinterpret_cast<float *>(ws);
     float *st_s = P + kItemBuf;
     unsigned *surv = reinterpret_cast<unsigned *>(st_s + SA);
@@ -376,11 +376,8 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
                         const int gk = off + k;
                         const TabView Tj{Tb, cell(surv[c + i]) << 4};
                         const ProjPatch pj = load_proj(projL + gk);
-#if SC_PPATH_GLOBAL_W
-                        P[k * G + i] = weak_eval(Tj, half_off, pj, a.w + gk * 9, a.bias[gk]);
-#else
-                        P[k * G + i] = weak_eval(Tj, half_off, pj, Wl + gk * 9, Bl[gk]);
-#endif
+                        P[k * G + i] = LW ? weak_eval(Tj, half_off, pj, Wl + gk * 9, Bl[gk])
+                                          : weak_eval(Tj, half_off, pj, a.w + gk * 9, a.bias[gk]);
                     }
                     wave_sync();
                     unsigned sv = 0;
@@ -505,19 +502,30 @@ __global__ __launch_bounds__(64) void walk_kernel(WalkArgs a) {
 
 int launch_cascade(const CascadeArgs &a, int device, hipStream_t s) {
     const int SA = (a.strip_max * a.band_rows + 63) & ~63;
-    const size_t lds = model_lds_bytes(a.K) + kWavesPerWg * wave_scratch_bytes(SA);
+    const size_t scratch = kWavesPerWg * wave_scratch_bytes(SA);
+    // weights in LDS whenever they fit: measured faster even where it costs
+    // occupancy (64x128 model, K = 380: 2 instead of 3 workgroups per CU, -2.5%)
+    bool lw = model_lds_bytes(a.K, true) + scratch <= 160 * 1024;
+    if (const char *e = std::getenv("SC_LDS_WEIGHTS")) lw = std::atoi(e) != 0;  // tuning override
+    const size_t lds = model_lds_bytes(a.K, lw) + scratch;
     static int cus = 0, dev_cached = -1;
     if (dev_cached != device) {
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         dev_cached = device;
     }
     int per_cu = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cascade_kernel, kCascadeThreads, lds);
+    if (lw)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cascade_kernel<true>, kCascadeThreads, lds);
+    else
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cascade_kernel<false>, kCascadeThreads, lds);
     per_cu = std::max(1, std::min(per_cu, 4));
     if (const char *e = std::getenv("SC_WGS_PER_CU"))  // tuning override
         per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
     const int grid = std::max(1, cus) * per_cu;
-    hipLaunchKernelGGL(cascade_kernel, dim3(grid), dim3(kCascadeThreads), lds, s, a);
+    if (lw)
+        hipLaunchKernelGGL(cascade_kernel<true>, dim3(grid), dim3(kCascadeThreads), lds, s, a);
+    else
+        hipLaunchKernelGGL(cascade_kernel<false>, dim3(grid), dim3(kCascadeThreads), lds, s, a);
     return grid;
 }
 
@@ -525,8 +533,9 @@ void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s) {
     hipLaunchKernelGGL(walk_kernel, dim3(a.n_rows * n_frames), dim3(64), 0, s, a);
 }
 
-size_t cascade_lds_bytes(int K, int strip_max, int band_rows) {
-    return model_lds_bytes(K) + kWavesPerWg * wave_scratch_bytes((strip_max * band_rows + 63) & ~63);
+size_t cascade_lds_bytes(int K, int strip_max, int band_rows) {  // smallest variant
+    return model_lds_bytes(K, false) +
+           kWavesPerWg * wave_scratch_bytes((strip_max * band_rows + 63) & ~63);
 }
 
 }  // namespace sc

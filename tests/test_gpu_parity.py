@@ -101,7 +101,10 @@ def test_grid_parity_kernel_paths(sc, oracle, face_cascade, monkeypatch, chunk_m
         assert T.view(np.uint32).tobytes() == oracle.integral(img).view(np.uint32).tobytes()
 
 
-def test_pedestrian_64x128(sc, oracle, ped_cascade):
+@pytest.mark.parametrize("lds_weights", [None, "0"])
+def test_pedestrian_64x128(sc, oracle, ped_cascade, monkeypatch, lds_weights):
+    if lds_weights:  # the cache-read weights variant (models too big for the LDS)
+        monkeypatch.setenv("SC_LDS_WEIGHTS", lds_weights)
     img = _frame(960, 540, 21)
     _grid_parity(sc, oracle, ped_cascade, PED_CFG, img,
                  sc.ScanParams.pedestrian(n_levels=12),
