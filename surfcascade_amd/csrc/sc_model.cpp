@@ -56,7 +56,6 @@ struct Parser {
                 i = e + 2;
                 continue;
             }
-            if (c == '@') fail("@include is not supported");
             return;
         }
     }
@@ -243,7 +242,45 @@ struct Parser {
 
 }  // namespace
 
-CfgValue cfg_parse(const std::string &text) {
+// libconfig's include directive (scanner.l: `^[ \t]*@include[ \t]+"file"`):
+// the named file's text replaces the line.  Model::Load sets no include
+// directory, so relative paths resolve against the working directory.
+std::string expand_includes(const std::string &text, int depth) {
+    if (text.find("@include") == std::string::npos) return text;
+    if (depth >= 10)  // libconfig's MAX_INCLUDE_DEPTH
+        throw Error{SC_ERR_PARSE, "@include nested too deeply"};
+    std::string out;
+    size_t pos = 0;
+    while (pos < text.size()) {
+        size_t eol = text.find('\n', pos);
+        if (eol == std::string::npos) eol = text.size();
+        const std::string ln = text.substr(pos, eol - pos);
+        size_t k = 0;
+        while (k < ln.size() && (ln[k] == ' ' || ln[k] == '\t')) k++;
+        if (ln.compare(k, 8, "@include") == 0) {
+            size_t q0 = ln.find('"', k + 8), q1 = q0 == std::string::npos ? q0 : ln.find('"', q0 + 1);
+            if (q1 == std::string::npos) throw Error{SC_ERR_PARSE, "bad @include line"};
+            const std::string path = ln.substr(q0 + 1, q1 - q0 - 1);
+            std::FILE *f = std::fopen(path.c_str(), "rb");
+            if (!f) throw Error{SC_ERR_PARSE, "cannot open include file '" + path + "'"};
+            std::string inc;
+            char buf[4096];
+            size_t n;
+            while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) inc.append(buf, n);
+            std::fclose(f);
+            out += expand_includes(inc, depth + 1);
+            out += ln.substr(q1 + 1);
+        } else {
+            out += ln;
+        }
+        if (eol < text.size()) out += '\n';
+        pos = eol + 1;
+    }
+    return out;
+}
+
+CfgValue cfg_parse(const std::string &text_in) {
+    const std::string text = expand_includes(text_in, 0);
     Parser p{text};
     CfgValue root;
     root.type = CfgValue::Group;

@@ -149,3 +149,24 @@ def test_mixed_array_types_rejected(sc):
     with pytest.raises(sc.SurfCascadeError) as e:
         sc.Model.parse(_mini(w=", ".join(["0.5"] * 32 + ["1"])))
     assert e.value.code == -3
+
+
+def test_include_directive(sc, tmp_path, monkeypatch):
+    """libconfig @include (scanner.l): the file's text replaces the line; Model::Load
+    sets no include dir, so the path resolves against the working directory."""
+    text = open(FACE_CFG).read()
+    lines = text.splitlines(keepends=True)
+    cut = len(lines) // 2
+    (tmp_path / "part2.cfg").write_text("".join(lines[cut:]))
+    (tmp_path / "part1.cfg").write_text("".join(lines[:cut]) + '  @include "part2.cfg"\n')
+    monkeypatch.chdir(tmp_path)
+    a, b = sc.CascadeClassifier(), sc.CascadeClassifier()
+    assert sc.Model(str(tmp_path / "part1.cfg")).Load(a) == sc.EXIT_SUCCESS
+    assert sc.Model(FACE_CFG).Load(b) == sc.EXIT_SUCCESS
+    for x, y in zip(_flat(a), _flat(b)):
+        np.testing.assert_array_equal(x, y)
+    (tmp_path / "loop.cfg").write_text('@include "loop.cfg"\n')
+    with pytest.raises(sc.SurfCascadeError):
+        sc.Model.parse('@include "loop.cfg"\n')
+    with pytest.raises(sc.SurfCascadeError):
+        sc.Model.parse('@include "missing.cfg"\n')
