@@ -117,6 +117,27 @@ int sc_enqueue_device(sc_detector *d, const uint8_t *d_frames, int n, int w,
 int sc_synchronize(sc_detector *d);
 void *sc_detector_stream(sc_detector *d); /* hipStream_t */
 
+/* ---- hard-negative mining (training side) ----------
+ * DenseSURFFeatureExtractor::FillNegSamples' scan of one negative image
+ * (DenseSURFFeatureExtractor.cpp:124-195): square windows l_k =
+ * (int)(tmpl_w * 1.1^k) for k = 0..(int)min(log(W/(float)tmpl_w)/log 1.1,
+ * log(H/(float)tmpl_w)/log 1.1), rows and columns at stride 10, no
+ * prefilter.  A window is a candidate (a false positive to train on) when
+ * the cascade accepts it (CascadeClassifier::Predict, CascadeClassifier.cpp:
+ * 63-72); m == NULL is the first round (no stage yet): every window is.
+ * The miner is an sc_detector; sc_detect* on it fail with SC_ERR_INVALID. */
+int sc_miner_create(const sc_model *m, int tmpl_w, int tmpl_h, int device,
+                    sc_detector **out);
+/* Candidates in (level, y, x) order -- the reference appends them from
+ * OpenMP threads in a nondeterministic order and stops at n_total.  The first
+ * `capacity` go to wins (stage_reached = number of stages, score = last
+ * stage score) and, when features != NULL, their ExtractFeatures descriptors
+ * over every template patch (sc_extract_patches order, CalcFeature +
+ * Normalize, :88-93, :379-457): float[capacity][n_patches][32].
+ * *n_out = all candidates; SC_ERR_CAPACITY when that exceeds capacity. */
+int sc_mine(sc_detector *d, const uint8_t *gray, int w, int h, int stride_bytes,
+            sc_window *wins, float *features, int capacity, int *n_out);
+
 /* ---- introspection / parity dumps -------------------------------------- */
 #define SC_INFO_LEVELS 1        /* levels used for the last geometry         */
 #define SC_INFO_GRID_WINDOWS 2  /* stride-step grid windows per frame        */

@@ -91,6 +91,10 @@ def lib():
                                        ctypes.POINTER(ScoModel), ctypes.POINTER(ScoParams),
                                        ctypes.c_void_p, ctypes.c_int64, _i64p, ctypes.c_int, _f32p]
         L.sco_detect_frame.restype = ctypes.c_int64
+        L.sco_mine.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ScoModel), _i32p,
+                               ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                               ctypes.c_int]
+        L.sco_mine.restype = ctypes.c_int64
         L.sco_group_rectangles.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_double, ctypes.c_void_p]
         L.sco_fddb_format.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int,
@@ -233,6 +237,29 @@ class Cascade:
         self._keep = arrs
         return ScoModel(self.n_stages, _p(arrs[0], _i32p), _p(arrs[1], _f32p), _p(arrs[2], _i32p),
                         _p(arrs[3], _f32p), _p(arrs[4], _f64p), self.tmpl_w, self.tmpl_h)
+
+
+def empty_cascade(tmpl_w=40, tmpl_h=40):
+    """A cascade with no stage yet: FillNegSamples' first round (first == true)."""
+    return Cascade(tmpl_w, tmpl_h, np.zeros(0, np.int32), np.zeros(0, np.float32),
+                   np.zeros(0, np.int32), np.zeros((0, 33), np.float32), np.zeros(0, np.float64))
+
+
+def mine(T, cascade: Cascade, cap, features=True, nthreads=8):
+    """FillNegSamples' scan of one image (sc_oracle.c sco_mine): (candidate
+    windows in (level, y, x) order -- the first cap --, their descriptors
+    [n, n_patches, 32] over all template patches, total candidate count)."""
+    T = np.ascontiguousarray(T, np.float32)
+    H, W = T.shape[0] - 1, T.shape[1] - 1
+    patches = np.ascontiguousarray(extract_patches(cascade.tmpl_w, cascade.tmpl_h), np.int32)
+    P = len(patches)
+    out = np.zeros(max(cap, 1), WINDOW_DTYPE)
+    feat = np.zeros((max(cap, 1), P, 32), np.float32) if features else None
+    m = cascade.c()
+    n = lib().sco_mine(_p(T, _f32p), W, H, ctypes.byref(m), _p(patches, _i32p), P, out.ctypes.data,
+                       feat.ctypes.data if features else None, cap, nthreads)
+    k = min(n, cap)
+    return out[:k].copy(), (feat[:k].copy() if features else None), int(n)
 
 
 def eval_grid(T, cascade: Cascade, params: Params, nthreads=8):

@@ -405,3 +405,64 @@ int64_t sco_detect_frame(const uint8_t *img, int W, int H, int stride,
     if (!scratch_T) free(T);
     return n;
 }
+
+/* Hard-negative scan of one image -- DenseSURFFeatureExtractor::FillNegSamples
+ * (DenseSURFFeatureExtractor.cpp:124-195): levels l_k = (int)(tw * 1.1^k),
+ * k = 0..(int)min(log(W/(float)tw)/log(1.1), log(H/(float)tw)/log(1.1))
+ * (:146, :153; the height term also divides by size.width), square l x l
+ * windows with rows and columns at stride 10 (:155, :161), no prefilter.  A
+ * window is a candidate when the cascade accepts it (CascadeClassifier::
+ * Predict, CascadeClassifier.cpp:63-72: no stage's GentleAdaboost::Predict is
+ * below its theta) -- with no stage yet ("first", :170) every window is.
+ * Candidates in (level, y, x) order; the first `cap` get their ExtractFeatures
+ * descriptors (:88-93) over all n_patches template patches, ProjectPatches'd
+ * to the window: feat[(i*n_patches + j)*32 + c].  The reference appends them
+ * from OpenMP threads in a nondeterministic order and stops at n_total; the
+ * candidate set is what is deterministic.  Returns the candidate count. */
+int64_t sco_mine(const float *T, int W, int H, const sco_model *m, const int32_t *patches,
+                 int n_patches, sco_window *out, float *feat, int64_t cap, int nthreads) {
+    const int tw = m->tmpl_w, nl = sco_num_levels(W, H, tw, tw);
+    if (nl <= 0) return 0;
+    sco_window **lv = (sco_window **)calloc((size_t)nl, sizeof(sco_window *));
+    int64_t *cnt = (int64_t *)calloc((size_t)nl, sizeof(int64_t));
+    int i;
+#pragma omp parallel for schedule(dynamic) num_threads(nthreads > 0 ? nthreads : 1)
+    for (i = 0; i < nl; i++) {
+        int l = sco_level_len(tw, i);
+        if (l > W || l > H) continue;
+        int64_t n = 0, c = (int64_t)((H - l) / 10 + 1) * ((W - l) / 10 + 1);
+        lv[i] = (sco_window *)malloc(sizeof(sco_window) * (size_t)c);
+        for (int y = 0; y <= H - l; y += 10)
+            for (int x = 0; x + l <= W; x += 10) {
+                float s_last = 0.0f;
+                int p = sco_eval_window(T, W, m, l, l, x, y, -INFINITY, &s_last, NULL);
+                if (p == m->n_stages) {
+                    sco_window wv = {i, x, y, l, l, p, (double)s_last};
+                    lv[i][n++] = wv;
+                }
+            }
+        cnt[i] = n;
+    }
+    int64_t total = 0;
+    for (i = 0; i < nl; i++) {
+        for (int64_t k = 0; k < cnt[i]; k++) {
+            if (total < cap) {
+                sco_window wv = lv[i][k];
+                if (out) out[total] = wv;
+                if (feat) {
+                    float scale = (float)wv.w / (float)tw;
+                    for (int j = 0; j < n_patches; j++) {
+                        int32_t pr[4];
+                        sco_project(patches + 4 * j, scale, wv.x, wv.y, pr);
+                        sco_calc_feature(T, W, pr, feat + ((size_t)total * n_patches + j) * 32);
+                    }
+                }
+            }
+            total++;
+        }
+        free(lv[i]);
+    }
+    free(lv);
+    free(cnt);
+    return total;
+}

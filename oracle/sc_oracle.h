@@ -92,6 +92,10 @@ int64_t sco_detect_frame(const uint8_t *img, int W, int H, int stride,
                          sco_window *out, int64_t cap, int64_t *n_visited,
                          int nthreads, float *scratch_T);
 
+/* Hard-negative scan of one image (FillNegSamples): candidates + descriptors. */
+int64_t sco_mine(const float *T, int W, int H, const sco_model *m, const int32_t *patches,
+                 int n_patches, sco_window *out, float *feat, int64_t cap, int nthreads);
+
 /* Post-processing (sc_oracle_group.c): groupRectangles + FDDB block. */
 typedef struct {
     int32_t x, y, w, h;

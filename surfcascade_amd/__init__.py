@@ -20,7 +20,7 @@ import numpy as np
 __all__ = ["ScanParams", "Model", "CascadeClassifier", "StageClassifier", "LogisticRegression",
            "Detector", "SurfCascadeError", "WINDOW_DTYPE", "RECORD_DTYPE", "library_path",
            "load_library", "extract_patches", "RECT_DTYPE", "groupRectangles", "group_detections",
-           "fddb_format"]
+           "fddb_format", "Miner"]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -49,6 +49,7 @@ EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_mode
            "sc_enqueue_device", "sc_synchronize", "sc_detector_stream", "sc_detector_info",
            "sc_detector_set_debug", "sc_debug_dump", "sc_set_timing", "sc_get_timing",
            "sc_group_rectangles", "sc_group_detections", "sc_fddb_format",
+           "sc_miner_create", "sc_mine",
            "sc_last_error", "sc_version")
 
 
@@ -139,6 +140,8 @@ def load_library():
     L.sc_debug_dump.argtypes = [vp, i32, i32, vp, sz]
     L.sc_set_timing.argtypes = [vp, i32]
     L.sc_get_timing.argtypes = [vp, P(ctypes.c_double), P(i64)]
+    L.sc_miner_create.argtypes = [vp, i32, i32, i32, P(vp)]
+    L.sc_mine.argtypes = [vp, vp, i32, i32, i32, vp, vp, i32, P(i32)]
     L.sc_group_rectangles.argtypes = [vp, i32, i32, ctypes.c_double, vp, i32, P(i32)]
     L.sc_group_detections.argtypes = [vp, i32, i32, i32, ctypes.c_double, vp, i32, vp, P(i32)]
     L.sc_fddb_format.argtypes = [ctypes.c_char_p, vp, i32, ctypes.c_char_p, sz, P(sz)]
@@ -426,3 +429,42 @@ class Detector:
         n = (ctypes.c_int64 * len(KERNELS))()
         _check(load_library().sc_get_timing(self._h, ms, n))
         return {k: (ms[i], n[i]) for i, k in enumerate(KERNELS)}
+
+
+class Miner(Detector):
+    """DenseSURFFeatureExtractor::FillNegSamples' scan (hard-negative mining):
+    every stride-10 window of levels tmpl_w * 1.1^k that the cascade accepts --
+    or every window when there is no cascade yet (the first round)."""
+
+    def __init__(self, cascade=None, tmpl_w=40, tmpl_h=40, device: int = 0):
+        L = load_library()
+        self.params = None
+        self.tmpl_w, self.tmpl_h = tmpl_w, tmpl_h
+        self._own = None
+        if cascade is not None and not isinstance(cascade, CascadeClassifier):
+            self._own = CascadeClassifier()
+            if Model(str(cascade)).Load(self._own) != EXIT_SUCCESS:
+                raise SurfCascadeError(-4, "cannot load model %s" % cascade)
+            cascade = self._own
+        h = ctypes.c_void_p()
+        _check(L.sc_miner_create(cascade._handle if cascade is not None else None, tmpl_w, tmpl_h,
+                                 device, ctypes.byref(h)))
+        self._h = h.value
+        self.device = device
+        self.n_patches = len(extract_patches(tmpl_w, tmpl_h))
+
+    def mine(self, img, capacity, features=True):
+        """-> (windows WINDOW_DTYPE in (level, y, x) order, descriptors
+        float32 [n, n_patches, 32] or None, total candidate count)."""
+        img = np.ascontiguousarray(img, np.uint8)
+        H, W = img.shape
+        wins = np.zeros(max(capacity, 1), WINDOW_DTYPE)
+        feat = np.zeros((max(capacity, 1), self.n_patches, 32), np.float32) if features else None
+        n = ctypes.c_int()
+        rc = load_library().sc_mine(self._h, img.ctypes.data, W, H, W, wins.ctypes.data,
+                                    feat.ctypes.data if features else None, capacity,
+                                    ctypes.byref(n))
+        if rc != -6:
+            _check(rc)
+        k = min(n.value, capacity)
+        return wins[:k].copy(), (feat[:k].copy() if features else None), n.value

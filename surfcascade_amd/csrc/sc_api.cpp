@@ -76,6 +76,7 @@ struct Geometry {
     std::vector<sc::LevelInfo> levels;
     std::vector<int2> rows;
     std::vector<sc::ProjPatch> proj;
+    std::vector<sc::ProjPatch> proj_all;  // miner: every template patch per level
     std::vector<sc::TaskDesc> tasks;
 };
 
@@ -100,6 +101,13 @@ struct sc_detector {
     DevBuf<sc::LevelInfo> d_levels;
     DevBuf<int2> d_rows;
     DevBuf<sc::ProjPatch> d_proj;
+    // hard-negative miner (FillNegSamples): stride 10, no prefilter, no walk
+    bool miner = false;
+    std::vector<int32_t> all_rects;  // every template patch (ExtractPatches)
+    DevBuf<sc::ProjPatch> d_proj_all;
+    DevBuf<int> d_mine_cnt, d_mine_off;
+    DevBuf<sc::MineWindow> d_mine_win;
+    DevBuf<float> d_feat;
     DevBuf<sc::TaskDesc> d_tasks;
     // working buffers
     DevBuf<uint8_t> d_frames;
@@ -137,6 +145,8 @@ struct sc_detector {
         for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
         d_w.release(); d_bias.release(); d_theta.release(); d_stage_off.release(); d_order.release();
         d_levels.release(); d_rows.release(); d_proj.release(); d_tasks.release();
+        d_proj_all.release(); d_mine_cnt.release(); d_mine_off.release(); d_mine_win.release();
+        d_feat.release();
         d_frames.release(); d_table.release(); d_carry.release(); d_out.release(); d_counters.release();
         d_visited.release(); d_queues.release(); d_st_p.release(); d_st_s.release();
         d_dbg_v.release();
@@ -222,8 +232,7 @@ void build_geometry(sc_detector *d, int W, int H) {
         // ProjectPatches (DenseSURFFeatureExtractor.cpp:459-484) + cell split
         // (GetRectsFromPatch :360-377) for every fitted patch at this level.
         const float scale = (float)L.l / (float)p.tmpl_w;
-        for (int k = 0; k < d->K; k++) {
-            const int32_t *r = &d->patch_rects[4 * k];
+        auto project = [&](const int32_t *r) {
             int px = (int)((float)r[0] * scale), py = (int)((float)r[1] * scale), pw, ph;
             if (r[2] >= r[3]) {
                 int ratio = r[2] / r[3];
@@ -254,8 +263,12 @@ void build_geometry(sc_detector *d, int W, int H) {
             pp.row0 = py * tg.rowp;
             pp.rowstep = c * tg.rowp;
             for (int q = 0; q <= gw; q++) pp.col[q] = col_off(px + q * c);
-            ng.proj[(size_t)i * d->K + k] = pp;
-        }
+            return pp;
+        };
+        for (int k = 0; k < d->K; k++) ng.proj[(size_t)i * d->K + k] = project(&d->patch_rects[4 * k]);
+        if (d->miner)  // ExtractFeatures over every template patch (:88-93)
+            for (size_t j = 0; j < d->all_rects.size() / 4; j++)
+                ng.proj_all.push_back(project(&d->all_rects[4 * j]));
         ng.levels.push_back(L);
     }
     ng.grid = gb;  // may be 0: no window fits (the reference loop runs 0 times)
@@ -317,6 +330,12 @@ void build_geometry(sc_detector *d, int W, int H) {
     if (!ng.proj.empty())
         HIPCHK(hipMemcpyAsync(d->d_proj.p, ng.proj.data(), ng.proj.size() * sizeof(sc::ProjPatch),
                               hipMemcpyHostToDevice, d->stream));
+    if (!ng.proj_all.empty()) {
+        d->d_proj_all.ensure(ng.proj_all.size());
+        HIPCHK(hipMemcpyAsync(d->d_proj_all.p, ng.proj_all.data(),
+                              ng.proj_all.size() * sizeof(sc::ProjPatch), hipMemcpyHostToDevice,
+                              d->stream));
+    }
     HIPCHK(hipStreamSynchronize(d->stream));  // host vectors are re-assigned below
     d->geo = std::move(ng);
 }
@@ -326,7 +345,8 @@ void upload_model(sc_detector *d) {
     d->S = (int)c.stages.size();
     d->K = c.total_weak();
     std::vector<int32_t> all = sc::extract_patches(d->prm.tmpl_w, d->prm.tmpl_h);
-    sc::validate_for_detect(c, (int)all.size() / 4);
+    if (!(d->miner && c.stages.empty()))  // a miner may run before the first stage
+        sc::validate_for_detect(c, (int)all.size() / 4);
     std::vector<float> w((size_t)d->K * 36, 0.0f);
     std::vector<double> bias(d->K);
     std::vector<float> theta(d->S);
@@ -381,14 +401,16 @@ void check_params(const sc_scan_params &p) {
         throw Error{SC_ERR_INVALID, "invalid scan parameters"};
 }
 
-sc_detector *make_detector(const sc::Cascade &c, const sc_scan_params *p, int device) {
+sc_detector *make_detector(const sc::Cascade &c, const sc_scan_params *p, int device,
+                           bool miner = false) {
     // host-side validation first: a bad model / parameter set is reported as
     // such even on a machine without a GPU
     sc_scan_params prm;
     if (p) prm = *p;
     else sc_scan_params_default(&prm);
     check_params(prm);
-    sc::validate_for_detect(c, (int)sc::extract_patches(prm.tmpl_w, prm.tmpl_h).size() / 4);
+    if (!(miner && c.stages.empty()))
+        sc::validate_for_detect(c, (int)sc::extract_patches(prm.tmpl_w, prm.tmpl_h).size() / 4);
     int ndev = 0;
     HIPCHK(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev)
@@ -405,6 +427,8 @@ sc_detector *make_detector(const sc::Cascade &c, const sc_scan_params *p, int de
         d->device = device;
         d->prm = prm;
         d->casc = c;
+        d->miner = miner;
+        if (miner) d->all_rects = sc::extract_patches(prm.tmpl_w, prm.tmpl_h);
         HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         upload_model(d);
     } catch (...) {
@@ -489,6 +513,8 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_WINDOWS, e0);
 
+    if (d->miner) return;  // FillNegSamples visits every window: no walk
+
     sc::WalkArgs wk{};
     wk.rows = d->d_rows.p;
     wk.levels = d->d_levels.p;
@@ -520,6 +546,7 @@ bool rec_less(const sc_det_record &a, const sc_det_record &b) {
 // Synchronous device-frame detection with host output.
 int detect_device_sync(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int stride,
                        sc_window *out, int capacity, int *n_out) {
+    if (d->miner) throw Error{SC_ERR_INVALID, "a miner scans with sc_mine, not sc_detect*"};
     if (n <= 0 || !d_frames || !n_out || (capacity > 0 && !out) || capacity < 0)
         throw Error{SC_ERR_INVALID, "bad arguments"};
     if (stride < W) throw Error{SC_ERR_INVALID, "stride smaller than width"};
@@ -548,6 +575,87 @@ int detect_device_sync(sc_detector *d, const uint8_t *d_frames, int n, int W, in
     }
     if (total > capacity) {
         g_err = "output capacity " + std::to_string(capacity) + " < " + std::to_string(total);
+        return SC_ERR_CAPACITY;
+    }
+    return SC_OK;
+}
+
+// FillNegSamples' scan of one device frame: the shared integral + cascade
+// kernels on the stride-10 grid, then candidate selection and descriptors.
+int mine_sync(sc_detector *d, const uint8_t *d_frame, int W, int H, int stride, sc_window *wins,
+              float *feat, int capacity, int *n_out) {
+    if (!d->miner) throw Error{SC_ERR_INVALID, "not a miner (sc_miner_create)"};
+    if (!d_frame || !n_out || capacity < 0 || (capacity > 0 && !wins))
+        throw Error{SC_ERR_INVALID, "bad arguments"};
+    if (stride < W) throw Error{SC_ERR_INVALID, "stride smaller than width"};
+    d->d_counters.ensure(2);
+    enqueue(d, d_frame, 1, W, H, stride, nullptr, 0, d->d_counters.p);
+    const Geometry &g = d->geo;
+    *n_out = 0;
+    if (g.grid == 0) {
+        HIPCHK(hipStreamSynchronize(d->stream));
+        return SC_OK;
+    }
+    const int nb = (int)((g.grid + sc::kMineBlock - 1) / sc::kMineBlock);
+    d->d_mine_cnt.ensure(nb);
+    d->d_mine_off.ensure(nb);
+    d->d_mine_win.ensure(std::max(capacity, 1));
+    sc::MineArgs ma{};
+    ma.st_p = d->d_st_p.p;
+    ma.st_s = d->d_st_s.p;
+    ma.grid = g.grid;
+    ma.n_stages = d->S;
+    ma.step = g.step;
+    ma.n_levels = g.n_levels;
+    ma.levels = d->d_levels.p;
+    ma.block_count = d->d_mine_cnt.p;
+    ma.block_offset = d->d_mine_off.p;
+    ma.out = d->d_mine_win.p;
+    ma.capacity = capacity;
+    sc::launch_mine_count(ma, d->stream);
+    HIPCHK(hipGetLastError());
+    std::vector<int> cnt(nb);
+    HIPCHK(hipMemcpyAsync(cnt.data(), d->d_mine_cnt.p, sizeof(int) * nb, hipMemcpyDeviceToHost,
+                          d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    long long total = 0;
+    for (int b = 0; b < nb; b++) {
+        const int c = cnt[b];
+        cnt[b] = (int)std::min<long long>(total, INT32_MAX);
+        total += c;
+    }
+    HIPCHK(hipMemcpyAsync(d->d_mine_off.p, cnt.data(), sizeof(int) * nb, hipMemcpyHostToDevice,
+                          d->stream));
+    sc::launch_mine_scatter(ma, d->stream);
+    HIPCHK(hipGetLastError());
+    const int kept = (int)std::min<long long>(total, capacity);
+    const int P = (int)d->all_rects.size() / 4;
+    if (feat && kept > 0) {
+        d->d_feat.ensure((size_t)kept * P * 32);
+        sc::FeatureArgs fa{};
+        fa.table = d->d_table.p;
+        fa.g = g.tg;
+        fa.windows = d->d_mine_win.p;
+        fa.n_windows = kept;
+        fa.n_patches = P;
+        fa.proj_all = d->d_proj_all.p;
+        fa.out = d->d_feat.p;
+        sc::launch_features(fa, d->stream);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(feat, d->d_feat.p, sizeof(float) * (size_t)kept * P * 32,
+                              hipMemcpyDeviceToHost, d->stream));
+    }
+    std::vector<sc::MineWindow> mw(kept);
+    if (kept > 0)
+        HIPCHK(hipMemcpyAsync(mw.data(), d->d_mine_win.p, sizeof(sc::MineWindow) * kept,
+                              hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    for (int i = 0; i < kept; i++)
+        wins[i] = sc_window{mw[i].level, mw[i].x, mw[i].y, mw[i].l, mw[i].l, d->S, (double)mw[i].score};
+    *n_out = (int)std::min<long long>(total, INT32_MAX);
+    if (total > capacity) {
+        g_err = "capacity " + std::to_string(capacity) + " < " + std::to_string(total) +
+                " candidates (the first " + std::to_string(capacity) + " were returned)";
         return SC_ERR_CAPACITY;
     }
     return SC_OK;
@@ -752,6 +860,35 @@ int sc_detect_device(sc_detector *d, const uint8_t *d_frames, int n, int w, int 
     });
 }
 
+int sc_miner_create(const sc_model *m, int tmpl_w, int tmpl_h, int device, sc_detector **out) {
+    return guarded([&] {
+        if (!out) throw Error{SC_ERR_INVALID, "null argument"};
+        sc_scan_params prm;
+        sc_scan_params_default(&prm);
+        prm.base_len = tmpl_w;  // l_k = (int)(size.width * 1.1^k)  (:153)
+        prm.step = 10;          // win.x/y += 10  (:155, :161)
+        prm.prefilter_k = -INFINITY;  // no prefilter: every grid window is scanned
+        prm.tmpl_w = tmpl_w;
+        prm.tmpl_h = tmpl_h;
+        prm.aspect_h = 1;       // Rect win(0, 0, l, l)  (:154)
+        *out = make_detector(m ? m->c : sc::Cascade{}, &prm, device, true);
+        return SC_OK;
+    });
+}
+
+int sc_mine(sc_detector *d, const uint8_t *gray, int w, int h, int stride, sc_window *wins,
+            float *features, int capacity, int *n_out) {
+    return guarded([&] {
+        if (!d || !gray) throw Error{SC_ERR_INVALID, "bad arguments"};
+        if (w < 2 || h < 2 || stride < w) throw Error{SC_ERR_INVALID, "bad frame geometry"};
+        HIPCHK(hipSetDevice(d->device));
+        d->d_frames.ensure((size_t)w * h);
+        HIPCHK(hipMemcpy2DAsync(d->d_frames.p, w, gray, stride, w, h, hipMemcpyHostToDevice,
+                                d->stream));
+        return mine_sync(d, d->d_frames.p, w, h, w, wins, features, capacity, n_out);
+    });
+}
+
 int sc_detect_batch(sc_detector *d, const uint8_t *const *frames, int n, int w, int h, int stride,
                     sc_window *out, int capacity, int *n_out) {
     return guarded([&] {
@@ -780,6 +917,7 @@ int sc_enqueue_device(sc_detector *d, const uint8_t *d_frames, int n, int w, int
         if (!d || !d_frames || n <= 0 || !d_counts || capacity < 0 || (capacity > 0 && !d_out))
             throw Error{SC_ERR_INVALID, "bad arguments"};
         if (w < 2 || h < 2 || stride < w) throw Error{SC_ERR_INVALID, "bad frame geometry"};
+        if (d->miner) throw Error{SC_ERR_INVALID, "a miner scans with sc_mine, not sc_enqueue_device"};
         HIPCHK(hipSetDevice(d->device));
         enqueue(d, d_frames, n, w, h, stride, d_out, capacity, d_counts);
         return SC_OK;

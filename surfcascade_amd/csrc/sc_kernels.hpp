@@ -128,6 +128,40 @@ struct WalkArgs {
     uint8_t *dbg_v;  // optional [frame][grid] visited flags
 };
 
+// Hard-negative mining (sc_mine.hip, FillNegSamples): candidate selection
+// over the cascade kernel's per-window results, then descriptors.
+constexpr int kMineBlock = 1024;  // grid windows per selection block
+
+struct MineWindow {
+    int level, x, y, l;
+    float score;  // last stage score
+};
+
+struct MineArgs {
+    const int8_t *st_p;
+    const float *st_s;
+    long long grid;
+    int n_stages, step, n_levels;
+    const LevelInfo *levels;
+    int *block_count;         // [blocks] candidates per block
+    const int *block_offset;  // [blocks] exclusive prefix
+    MineWindow *out;
+    int capacity;
+};
+
+struct FeatureArgs {
+    const float4 *table;  // frame 0's table
+    TableGeom g;
+    const MineWindow *windows;
+    int n_windows, n_patches;
+    const ProjPatch *proj_all;  // [n_levels][n_patches]: every template patch projected
+    float *out;                 // [n_windows][n_patches][32]
+};
+
+void launch_mine_count(const MineArgs &a, hipStream_t s);
+void launch_mine_scatter(const MineArgs &a, hipStream_t s);
+void launch_features(const FeatureArgs &a, hipStream_t s);
+
 // integral pass 1 (rowcarry) and pass 2 (colstrip), sc_integral.hip
 void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s);
 void launch_colscan(const RowScanArgs &a, int n_frames, hipStream_t s);

@@ -1,0 +1,79 @@
+"""Hard-negative mining scan (DenseSURFFeatureExtractor::FillNegSamples,
+DenseSURFFeatureExtractor.cpp:124-195) through the C ABI against the oracle
+(oracle/sc_oracle.c sco_mine): candidate windows in (level, y, x) order and
+their 608 x 32 descriptors, bit-exact."""
+import numpy as np
+import pytest
+
+from conftest import FACE_CFG, PED_CFG
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sc():
+    import surfcascade_amd as sc
+    return sc
+
+
+def _frame(W, H, seed):
+    from surfcascade_amd import synth
+    return synth.make_frame(W, H, seed)
+
+
+def _win(a):
+    return [(int(r["level"]), int(r["x"]), int(r["y"]), int(r["w"]), int(r["h"])) for r in a]
+
+
+def _check(got, ref):
+    gw, gf, gn = got
+    rw, rf, rn = ref
+    assert gn == rn
+    assert _win(gw) == _win(rw)
+    assert gw["score"].astype(np.float32).tobytes() == rw["score"].astype(np.float32).tobytes()
+    if rf is not None:
+        assert gf.view(np.uint32).tobytes() == rf.view(np.uint32).tobytes()
+
+
+@pytest.mark.parametrize("W,H,seed", [(320, 240, 3), (401, 233, 8)])
+def test_first_round_every_window(sc, oracle, W, H, seed):
+    """No stage yet (first == true): every stride-10 window is a candidate."""
+    img = _frame(W, H, seed)
+    m = sc.Miner(None)
+    got = m.mine(img, 96)
+    ref = oracle.mine(oracle.integral(img), oracle.empty_cascade(), 96)
+    _check(got, ref)
+    assert got[2] > 96  # capacity path: the first 96 in order, total reported
+
+
+def test_with_cascade(sc, oracle, face_cascade):
+    from surfcascade_amd import synth
+    c = face_cascade
+    theta = np.full(c.n_stages, 0.42, np.float32)  # ~1300 candidates
+    text = synth.write_cfg(synth.cascade_tree(c.n_weak, theta, c.patch_index, c.w, c.bias))
+    img = _frame(480, 360, 17)
+    casc_or = oracle.cascade_from_cfg(text)
+    m = sc.Miner(sc.Model.parse(text))
+    wins, feat, n = m.mine(img, 4096, features=False)
+    rw, _, rn = oracle.mine(oracle.integral(img), casc_or, 4096, features=False)
+    assert 0 < n == rn < 4096
+    assert _win(wins) == _win(rw)
+    _check(m.mine(img, 40), oracle.mine(oracle.integral(img), casc_or, 40))
+
+
+def test_calibrated_model_and_tall_template(sc, oracle, face_cascade):
+    img = _frame(360, 300, 23)
+    T = oracle.integral(img)
+    _check(sc.Miner(FACE_CFG).mine(img, 32), oracle.mine(T, face_cascade, 32))
+    # FillNegSamples scans square l x l windows (Rect win(0, 0, l, l), :154): a 64x128
+    # template's patches project below such a window (the reference would read past
+    # it); the miner rejects that geometry instead of reading out of bounds
+    with pytest.raises(sc.SurfCascadeError) as e:
+        sc.Miner(PED_CFG, 64, 128).mine(img, 16)
+    assert e.value.code == -1 and "leaves the window" in str(e.value)
+
+
+def test_miner_is_not_a_detector(sc):
+    m = sc.Miner(None)
+    with pytest.raises(sc.SurfCascadeError):
+        m.detect(_frame(200, 200, 1))

@@ -368,3 +368,26 @@ def test_prefilter_numpy_matches_c(oracle):
                                                  j * st, r * st, l, lh, 6.0, None)
                 assert bool(got) == pm[k]
                 k += 1
+
+
+def test_mine_first_round_counts_every_stride10_window(oracle):
+    """FillNegSamples (DenseSURFFeatureExtractor.cpp:146-161): with no stage
+    every l x l window at stride 10 is a candidate, l = (int)(40 * 1.1^k)."""
+    import math
+    from surfcascade_amd import synth
+    W, H = 333, 251
+    T = oracle.integral(synth.make_frame(W, H, 4))
+    nl = int(min(math.log(np.float32(W / np.float32(40))) / math.log(1.1),
+                 math.log(np.float32(H / np.float32(40))) / math.log(1.1)))
+    exp = sum(((H - l) // 10 + 1) * ((W - l) // 10 + 1)
+              for l in (int(40 * 1.1 ** k) for k in range(nl + 1)) if l <= min(W, H))
+    wins, feat, n = oracle.mine(T, oracle.empty_cascade(), 5)
+    assert n == exp
+    assert [tuple(w)[:5] for w in wins] == [(0, x, 0, 40, 40) for x in range(0, 50, 10)]
+    # descriptor of window 0, patch 0 == CalcFeature of the patch itself
+    r = oracle.extract_patches(40, 40)[0]
+    f = np.zeros(32, np.float32)
+    oracle.lib().sco_calc_feature(oracle._p(T, oracle._f32p), W,
+                                  oracle._p(np.ascontiguousarray(r, np.int32), oracle._i32p),
+                                  oracle._p(f, oracle._f32p))
+    assert feat[0, 0].tobytes() == f.tobytes()
