@@ -16,6 +16,7 @@
 #ifndef SURFCASCADE_HPP
 #define SURFCASCADE_HPP
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <memory>
@@ -203,6 +204,50 @@ class Detector {
     struct Free {
         void operator()(sc_detector *d) const { sc_detector_destroy(d); }
     };
+    std::unique_ptr<sc_detector, Free> det_;
+};
+
+// Hard-negative mining (DenseSURFFeatureExtractor::FillNegSamples,
+// DenseSURFFeatureExtractor.cpp:124-195) on the GPU: cascade == nullptr is
+// the first round (every stride-10 window is a candidate).
+class Miner {
+   public:
+    explicit Miner(const CascadeClassifier *cascade, int tmpl_w = 40, int tmpl_h = 40,
+                   int device = 0)
+        : n_patches_(sc_extract_patches(tmpl_w, tmpl_h, nullptr, 0)) {
+        sc_detector *d = nullptr;
+        check(sc_miner_create(cascade ? cascade->handle() : nullptr, tmpl_w, tmpl_h, device, &d));
+        det_.reset(d);
+    }
+    // One negative image: appends the descriptors (features_img: n_patches x
+    // 32, as ExtractFeatures fills it) of its candidates, in (level, y, x)
+    // order, until features_all holds n_total samples; true once it does.
+    bool FillNegSamples(const uint8_t *gray, int w, int h, int stride,
+                        std::vector<std::vector<std::vector<float>>> &features_all, size_t n_total) {
+        if (features_all.size() >= n_total) return true;
+        const int want = (int)(n_total - features_all.size());
+        std::vector<sc_window> wins(want);
+        std::vector<float> feat((size_t)want * n_patches_ * 32);
+        int n = 0;
+        const int rc = sc_mine(det_.get(), gray, w, h, stride, wins.data(), feat.data(), want, &n);
+        if (rc != SC_ERR_CAPACITY) check(rc);
+        const int kept = std::min(n, want);
+        for (int i = 0; i < kept; i++) {
+            std::vector<std::vector<float>> sample(n_patches_);
+            for (int j = 0; j < n_patches_; j++) {
+                const float *f = &feat[((size_t)i * n_patches_ + j) * 32];
+                sample[j].assign(f, f + 32);
+            }
+            features_all.push_back(std::move(sample));
+        }
+        return features_all.size() >= n_total;
+    }
+
+   private:
+    struct Free {
+        void operator()(sc_detector *d) const { sc_detector_destroy(d); }
+    };
+    int n_patches_;
     std::unique_ptr<sc_detector, Free> det_;
 };
 

@@ -43,6 +43,10 @@ int main(int argc, char **argv) {
         std::vector<int> weights(wins.size(), 0);  // ObjDetector.cpp:223-225
         surfcascade::groupRectangles(wins, weights, scores, 2, 0.2);
         std::printf("%s", surfcascade::FddbBlock("frame", wins, scores).c_str());
+        surfcascade::Miner miner(nullptr);  // first round: every stride-10 window
+        std::vector<std::vector<std::vector<float>>> negs;
+        const bool full = miner.FillNegSamples(img.data(), w, h, w, negs, 5);
+        std::printf("mined %zu %d %.9g\n", negs.size(), (int)full, negs.empty() ? 0.0 : negs[4][607][31]);
     }
     return 0;
 }
