@@ -149,7 +149,9 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
 /* Enable per-window debug records (grid order) for the next detect calls. */
 int sc_detector_set_debug(sc_detector *d, int on);
 #define SC_DUMP_INTEGRAL 1    /* float[(H+1)*(W+1)*8] of frame `frame`       */
-#define SC_DUMP_GRID_STAGE 2  /* int16[grid]: p (-1 = prefilter reject)      */
+#define SC_DUMP_GRID_STAGE 2  /* int16[grid]: p (-1 = prefilter reject, -2 =  */
+                              /* not evaluated: the default lazy grid only   */
+                              /* evaluates windows the x chain reaches)      */
 #define SC_DUMP_GRID_SCORE 3  /* float[grid]: last stage score               */
 #define SC_DUMP_GRID_VISIT 4  /* uint8[grid]: 1 = visited by the x chain     */
 int sc_debug_dump(sc_detector *d, int what, int frame, void *dst,

@@ -96,6 +96,7 @@ struct sc_detector {
     DevBuf<int> d_stage_off;
     DevBuf<int16_t> d_order;      // per stage: weak indices sorted by patch shape
     int chunk_min = 1 << 30;  // one-lane-per-window stages only when n > item buffer
+    bool lazy = true;         // chain kernel: only windows the x chain reaches are evaluated
     // geometry on device
     Geometry geo;
     DevBuf<sc::LevelInfo> d_levels;
@@ -118,6 +119,7 @@ struct sc_detector {
     DevBuf<int> d_counters;
     DevBuf<unsigned> d_visited;  // per (frame, row): windows the x chain visited
     DevBuf<int> d_queues;       // per-XCD task counters of the cascade kernel
+    DevBuf<int> d_entry;        // chain kernel: per (row, segment) chain entry + 1
     DevBuf<int8_t> d_st_p;      // per grid window: stage reached (-1 prefilter reject)
     DevBuf<float> d_st_s;       // per grid window: last stage score
     // debug
@@ -148,7 +150,7 @@ struct sc_detector {
         d_proj_all.release(); d_mine_cnt.release(); d_mine_off.release(); d_mine_win.release();
         d_feat.release();
         d_frames.release(); d_table.release(); d_carry.release(); d_out.release(); d_counters.release();
-        d_visited.release(); d_queues.release(); d_st_p.release(); d_st_s.release();
+        d_visited.release(); d_queues.release(); d_entry.release(); d_st_p.release(); d_st_s.release();
         d_dbg_v.release();
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -383,6 +385,8 @@ void upload_model(sc_detector *d) {
     }
     if (d->K > 32767) throw Error{SC_ERR_MODEL, "more than 32767 weak classifiers"};
     if (const char *e = std::getenv("SC_CHUNK_MIN")) d->chunk_min = std::max(1, std::atoi(e));
+    if (const char *e = std::getenv("SC_FULL_GRID")) d->lazy = std::atoi(e) == 0;  // A/B, dumps
+    if (d->miner) d->lazy = false;  // FillNegSamples evaluates every window
     d->d_w.ensure(w.size());
     d->d_bias.ensure(bias.size());
     d->d_theta.ensure(theta.size());
@@ -508,11 +512,14 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     ca.st_p = d->d_st_p.p;
     ca.st_s = d->d_st_s.p;
     HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kXcds * sc::kQueueStride, d->stream));
-    timed_begin(d, &e0);
-    sc::launch_cascade(ca, d->device, d->stream);
-    HIPCHK(hipGetLastError());
-    timed_end(d, SC_KERNEL_WINDOWS, e0);
-
+    const int seg_max = (g.nx_max + sc::kXcds - 1) / sc::kXcds;  // chain kernel segments
+    const bool lazy = d->lazy && sc::chain_lds_bytes(d->K, seg_max) <= 160 * 1024;
+    if (!lazy) {
+        timed_begin(d, &e0);
+        sc::launch_cascade(ca, d->device, d->stream);
+        HIPCHK(hipGetLastError());
+        timed_end(d, SC_KERNEL_WINDOWS, e0);
+    }
     if (d->miner) return;  // FillNegSamples visits every window: no walk
 
     sc::WalkArgs wk{};
@@ -530,10 +537,42 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     wk.counters = d_counts;
     wk.row_visited = d->d_visited.p;
     wk.dbg_v = d->debug ? d->d_dbg_v.p : nullptr;
+    wk.row_max = seg_max;
+    if (lazy) {  // the walk drives the cascade: one chain kernel
+        const size_t n_tasks = g.rows.size() * (size_t)n;
+        d->d_entry.ensure(n_tasks * sc::kXcds + 1);
+        wk.entry = d->d_entry.p;
+        wk.err = d->d_entry.p + n_tasks * sc::kXcds;  // zeroed with the entries
+        HIPCHK(hipMemsetAsync(d->d_entry.p, 0, sizeof(int) * (n_tasks * sc::kXcds + 1), d->stream));
+        HIPCHK(hipMemsetAsync(d->d_visited.p, 0, sizeof(unsigned) * n_tasks, d->stream));
+        if (d->debug) {  // dumps: unevaluated windows read -2, unvisited 0
+            HIPCHK(hipMemsetAsync(d->d_st_p.p, 0xFE, (size_t)g.grid * n, d->stream));
+            HIPCHK(hipMemsetAsync(d->d_st_s.p, 0, sizeof(float) * (size_t)g.grid * n, d->stream));
+            HIPCHK(hipMemsetAsync(d->d_dbg_v.p, 0, (size_t)g.grid * n, d->stream));
+        } else {
+            ca.st_p = nullptr;
+            ca.st_s = nullptr;
+        }
+        timed_begin(d, &e0);
+        sc::launch_chain(ca, wk, d->device, d->stream);
+        HIPCHK(hipGetLastError());
+        timed_end(d, SC_KERNEL_WINDOWS, e0);
+        return;
+    }
     timed_begin(d, &e0);
     sc::launch_walk(wk, n, d->stream);
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_WALK, e0);
+}
+
+// The chain kernel's hand-off watchdog (reads after the stream has drained).
+void check_chain(sc_detector *d) {
+    if (!d->lazy || d->d_entry.n == 0) return;
+    const size_t n_tasks = d->geo.rows.size() * (size_t)d->last_frames;
+    if (d->d_entry.n < n_tasks * sc::kXcds + 1) return;
+    int err = 0;
+    HIPCHK(hipMemcpy(&err, d->d_entry.p + n_tasks * sc::kXcds, sizeof(int), hipMemcpyDeviceToHost));
+    if (err) throw Error{SC_ERR_DEVICE, "chain kernel: " + std::to_string(err) + " segment hand-off(s) timed out"};
 }
 
 bool rec_less(const sc_det_record &a, const sc_det_record &b) {
@@ -562,6 +601,7 @@ int detect_device_sync(sc_detector *d, const uint8_t *d_frames, int n, int W, in
         if ((size_t)counts[0] <= cap_dev) break;
         cap_dev = (size_t)counts[0];
     }
+    check_chain(d);
     const int total = counts[0];
     std::vector<sc_det_record> recs(total);
     if (total > 0)
@@ -928,6 +968,7 @@ int sc_synchronize(sc_detector *d) {
     return guarded([&] {
         if (!d) throw Error{SC_ERR_INVALID, "null detector"};
         HIPCHK(hipStreamSynchronize(d->stream));
+        check_chain(d);
         return SC_OK;
     });
 }

@@ -126,6 +126,9 @@ struct WalkArgs {
     int *counters;  // [0] total, [1+f] per frame
     unsigned *row_visited;  // [frame][row] windows the x chain visited
     uint8_t *dbg_v;  // optional [frame][grid] visited flags
+    int row_max;     // chain kernel: most windows in one row segment (LDS sizing)
+    int *entry;      // chain kernel: [frame*rows][kXcds] chain entry + 1 per segment (zeroed)
+    int *err;        // chain kernel: hand-off timeouts (must stay 0)
 };
 
 // Hard-negative mining (sc_mine.hip, FillNegSamples): candidate selection
@@ -168,6 +171,11 @@ void launch_colscan(const RowScanArgs &a, int n_frames, hipStream_t s);
 // returns the number of workgroups launched
 int launch_cascade(const CascadeArgs &a, int device, hipStream_t s);
 void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s);
+// Lazy grid: the walk drives the cascade (chain kernel, sc_windows.hip); the
+// cascade args' st_p / st_s, when not null, receive the evaluated windows
+// (others keep the caller's fill).  Returns the number of workgroups.
+int launch_chain(const CascadeArgs &a, const WalkArgs &w, int device, hipStream_t s);
+size_t chain_lds_bytes(int K, int seg_max);
 size_t cascade_lds_bytes(int K, int strip_max, int band_rows);
 
 }  // namespace sc

@@ -43,6 +43,14 @@ namespace {
 #define SC_CASCADE_MIN_WGS 1
 #endif
 
+#ifndef SC_CHAIN_MIN_WGS  // chain kernel: 3 workgroups (12 waves) per CU
+#define SC_CHAIN_MIN_WGS 3
+#endif
+
+#ifndef SC_ABL_NOWAIT  // timing ablation only: segments start without the hand-off (wrong results)
+#define SC_ABL_NOWAIT 0
+#endif
+
 #ifndef SC_ITEM_BUF  // per-wave LDS results of the (survivor, weak) item path
 #define SC_ITEM_BUF 640
 #endif
@@ -82,31 +90,182 @@ __host__ __device__ inline size_t model_lds_bytes(int K, bool LW) {
     return (LW ? (size_t)K * 144 + (size_t)K * 8 : 0) + (((size_t)K * 2 + 15) & ~(size_t)15);
 }
 
+// A set of windows of one level: nr rows of nw windows; window (r, u) has
+// its origin cell (phase 0, half 0) at t_off + r*row_cells + u*wstep.
+struct WinSet {
+    unsigned t_off;
+    int nw, nr, row_cells, wstep;
+    int level;
+    float thr;  // prefilter threshold (ObjDetector.cpp:188)
+    int pre_row, pre_col;
+};
+
+// The per-window work of the detect loop for the windows `need(slot)`
+// selects: prefilter, then the cascade stage by stage over compacted
+// survivors.  Results in LDS: st_p[slot] = stage reached (-1: prefilter
+// reject), st_s[slot] = last stage score, slot = r*nw + u.
+//   1) prefilter: sum(win) > area*6 (DenseSURFFeatureExtractor.cpp:351-358,
+//      ObjDetector.cpp:188); survivors compacted in order (__ballot + popc).
+//   2) each stage (ObjDetector.cpp:193-199): (survivor, weak) items over the
+//      lanes in shape-sorted weak order, results through LDS, each survivor's
+//      lane adds them in the model's k order (GentleAdaboost.cpp:255-258);
+//      the theta test (:197) and order-preserving compaction.
+template <bool LW, class Need>
+__device__ __forceinline__ void eval_windows(const CascadeArgs &a, const WinSet &B, const char *Tb,
+                                             const float4 *Wl, const double *Bl, const int16_t *Ol,
+                                             float *P, float *st_s, unsigned *surv, int8_t *st_p,
+                                             int lane, Need need) {
+    const int K = a.K, half_off = a.g.hs;
+    const int nw = B.nw;
+    const float4 *T = reinterpret_cast<const float4 *>(Tb) + B.t_off;
+    // a survivor is (r << 16 | u); its LDS slot r*nw + u
+    auto cell = [&](unsigned sv) {
+        return B.t_off + (sv >> 16) * B.row_cells + (sv & 0xffffu) * B.wstep;
+    };
+    auto slot = [&](unsigned sv) { return (int)(sv >> 16) * nw + (int)(sv & 0xffffu); };
+
+    // 1) prefilter; survivors in (row, x) order
+    int nsurv = 0;
+    for (int r = 0; r < B.nr; r++) {
+        for (int b = 0; b < nw; b += 64) {
+            const int u = b + lane;
+            bool pass = false;
+            if (u < nw && need(r * nw + u)) {
+                const float4 *t0 = T + r * B.row_cells + u * B.wstep;
+                const float4 v = box4(t0[0], t0[B.pre_row + B.pre_col], t0[B.pre_col], t0[B.pre_row]);
+                const float m = (((v.x + v.y) + v.z) + v.w) / 2.0f;  // sum(), :351-358
+                pass = m > B.thr;                                    // ObjDetector.cpp:188
+                st_p[r * nw + u] = pass ? 0 : -1;
+                st_s[r * nw + u] = 0.0f;
+            }
+            const unsigned long long mk = __ballot(pass);
+            if (pass) surv[nsurv + __popcll(mk & lanes_below())] = ((unsigned)r << 16) | (unsigned)u;
+            nsurv += __popcll(mk);
+        }
+    }
+    wave_sync();
+
+    // 2) cascade, stage by stage over the compacted survivors
+    const ProjPatch *projL = a.proj + (long long)B.level * K;
+    for (int s = 0; s < a.n_stages && nsurv > 0; s++) {
+        const int off = a.stage_off[s], n = a.stage_off[s + 1] - off;
+        const float th = a.theta[s];
+        int nn = 0;
+        // stage decision of one survivor (GentleAdaboost.cpp:259;
+        // ObjDetector.cpp:197) and in-place order-preserving compaction:
+        // kept survivors move to [nn, ...), never past the group just read
+        auto decide = [&](bool valid, unsigned sv, float sum) {
+            bool keep = false;
+            if (valid) {
+                const float sc = sum / (float)n;
+                const int li = slot(sv);
+                st_s[li] = sc;
+                keep = !((double)sc < (double)th);
+                st_p[li] = (int8_t)(keep ? s + 1 : s);
+            }
+            const unsigned long long mk = __ballot(keep);
+            wave_sync();
+            if (keep) surv[nn + __popcll(mk & lanes_below())] = sv;
+            nn += __popcll(mk);
+            wave_sync();
+        };
+        if (nsurv >= a.chunk_min || n > kItemBuf) {
+            // one lane per survivor, k wave-uniform: parameters via scalar loads
+            for (int c = 0; c < nsurv; c += 64) {
+                const int i = c + lane;
+                unsigned sv = 0;
+                float sum = 0.0f;
+                if (i < nsurv) {
+                    sv = surv[i];
+                    const TabView Tj{Tb, cell(sv) << 4};
+                    for (int k = 0; k < n; k++) {
+                        const int gk = off + k;
+                        sum += weak_eval(Tj, half_off, projL[gk], a.w + gk * 9, a.bias[gk]);
+                    }
+                }
+                decide(i < nsurv, sv, sum);
+            }
+        } else {
+            // (survivor, weak) items over the lanes, groups of G survivors
+            // whose n*G results fit the wave's LDS buffer.  Items run in
+            // shape-sorted weak order (Ol: few patch shapes per wave
+            // instruction, so little divergence); each survivor's lane then
+            // adds its results in the reference's k order.
+            const int gcap = min(64, kItemBuf / n);
+            for (int c = 0; c < nsurv; c += gcap) {
+                const int G = min(gcap, nsurv - c), items = G * n;
+                const float rcp = 1.0f / (float)G;
+                auto decode = [&](int t2, int &k, int &i) {  // item -> (weak k, survivor i)
+                    int kk = (int)((float)t2 * rcp);                // kk = t2 / G
+                    i = t2 - kk * G;
+                    if (i < 0) { kk--; i += G; }
+                    else if (i >= G) { kk++; i -= G; }
+                    k = Ol[off + kk];
+                };
+                for (int t2 = lane; t2 < items; t2 += 64) {
+                    int k, i;
+                    decode(t2, k, i);
+                    const int gk = off + k;
+                    const TabView Tj{Tb, cell(surv[c + i]) << 4};
+                    const ProjPatch pj = load_proj(projL + gk);
+                    P[k * G + i] = LW ? weak_eval(Tj, half_off, pj, Wl + gk * 9, Bl[gk])
+                                      : weak_eval(Tj, half_off, pj, a.w + gk * 9, a.bias[gk]);
+                }
+                wave_sync();
+                unsigned sv = 0;
+                float acc = 0.0f;  // GentleAdaboost.cpp:255-258 order
+                if (lane < G) {
+                    sv = surv[c + lane];
+                    for (int k = 0; k < n; k++) acc += P[k * G + lane];
+                }
+                decide(lane < G, sv, acc);
+            }
+        }
+        nsurv = nn;
+    }
+}
+
+// The model staged in LDS once per persistent workgroup (the only
+// workgroup barrier: the waves are independent afterwards).
 template <bool LW>
-__global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_kernel(CascadeArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int K = a.K;
-    float4 *Wl = reinterpret_cast<float4 *>(smem);
-    double *Bl = reinterpret_cast<double *>(smem + (LW ? (size_t)K * 144 : 0));
-    int16_t *Ol = reinterpret_cast<int16_t *>(Bl + (LW ? K : 0));
+__device__ __forceinline__ void stage_model(const CascadeArgs &a, unsigned char *smem, float4 *&Wl,
+                                            double *&Bl, int16_t *&Ol) {
+    const int K = a.K, tid = threadIdx.x;
+    Wl = reinterpret_cast<float4 *>(smem);
+    Bl = reinterpret_cast<double *>(smem + (LW ? (size_t)K * 144 : 0));
+    Ol = reinterpret_cast<int16_t *>(Bl + (LW ? K : 0));
     if (LW)
         for (int i = tid; i < K * 9; i += kCascadeThreads) Wl[i] = a.w[i];
     for (int i = tid; i < K; i += kCascadeThreads) {
         if (LW) Bl[i] = a.bias[i];
         Ol[i] = a.order[i];
     }
-    __syncthreads();  // the only workgroup barrier: model staged, waves now independent
+    __syncthreads();
+}
+
+// Full-grid cascade: every window of the stride-`step` grid is evaluated
+// (parity dumps, FillNegSamples' scan).  Persistent workgroups of 4
+// independent waves; a task is one strip of a band of rows (sc_kernels.hpp),
+// XCD x serving the strips [x*n_sub, (x+1)*n_sub) of every band from its own
+// queue (steals from the others when empty): the table rows its L2 sees stay
+// in a narrow column band.
+template <bool LW>
+__global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_kernel(CascadeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float4 *Wl;
+    double *Bl;
+    int16_t *Ol;
+    stage_model<LW>(a, smem, Wl, Bl, Ol);
 
     const int SA = (a.strip_max * a.band_rows + 63) & ~63;
-    unsigned char *ws = smem + model_lds_bytes(K, LW) + (size_t)wv * wave_scratch_bytes(SA);
+    unsigned char *ws = smem + model_lds_bytes(a.K, LW) + (size_t)wv * wave_scratch_bytes(SA);
     float *P = reinterpret_cast<float *>(ws);
     float *st_s = P + kItemBuf;
     unsigned *surv = reinterpret_cast<unsigned *>(st_s + SA);
     int8_t *st_p = reinterpret_cast<int8_t *>(surv + SA);
 
     const TableGeom g = a.g;
-    const int half_off = g.hs, cs = g.cs, row_cells = g.step * g.rowp;
     const int n_tasks = a.n_frames * a.n_bands * a.n_sub, nseg = kXcds * a.n_sub;
     int q = (int)xcc_id(), empty = 0;
     // dequeue: one atomic per task on this XCD's queue word; the next task's
@@ -141,134 +300,22 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
         int tn = 0;  // prefetch the next task index
         if (lane == 0) tn = atomicAdd(&a.queues[q * kQueueStride], 1);
         const int frame = tf.y;
-        const int nw = D.nw, nr = D.nr;
-        if (nw <= 0) {  // empty strip (narrow row)
-            t = __builtin_amdgcn_readfirstlane(tn);
-            if (t < n_tasks) {
-                tf = task_index(t);
-                D = a.tasks[tf.x];
-            }
-            continue;
-        }
-        // the frame's table; window (r, u) of the band has its origin cell
-        // (phase 0, half 0) at D.t_off + r*row_cells + u
-        const char *Tb = reinterpret_cast<const char *>(a.table + (long long)frame * g.frame4);
-        const float4 *T = a.table + (long long)frame * g.frame4 + D.t_off;
-        // a survivor is (r << 16 | u); its LDS slot r*nw + u
-        auto cell = [&](unsigned sv) {
-            return (unsigned)D.t_off + (sv >> 16) * row_cells + (sv & 0xffffu) * cs;
-        };
-        auto slot = [&](unsigned sv) { return (int)(sv >> 16) * nw + (int)(sv & 0xffffu); };
-
-        // 1) prefilter; survivors in (row, x) order
-        int nsurv = 0;
-        for (int r = 0; r < nr; r++) {
-            for (int b = 0; b < nw; b += 64) {
-                const int u = b + lane;
-                bool pass = false;
-                if (u < nw) {
-                    const float4 *t0 = T + r * row_cells + u * cs;
-                    const float4 v = box4(t0[0], t0[D.pre_row + D.pre_col], t0[D.pre_col], t0[D.pre_row]);
-                    const float m = (((v.x + v.y) + v.z) + v.w) / 2.0f;  // sum(), :351-358
-                    pass = m > D.thr;                                    // ObjDetector.cpp:188
-                    st_p[r * nw + u] = pass ? 0 : -1;
-                    st_s[r * nw + u] = 0.0f;
-                }
-                const unsigned long long mk = __ballot(pass);
-                if (pass) surv[nsurv + __popcll(mk & lanes_below())] = ((unsigned)r << 16) | (unsigned)u;
-                nsurv += __popcll(mk);
-            }
-        }
-        wave_sync();
-
-        // 2) cascade, stage by stage over the compacted survivors
-        const ProjPatch *projL = a.proj + (long long)D.level * K;
-        for (int s = 0; s < a.n_stages && nsurv > 0; s++) {
-            const int off = a.stage_off[s], n = a.stage_off[s + 1] - off;
-            const float th = a.theta[s];
-            int nn = 0;
-            // stage decision of one survivor (GentleAdaboost.cpp:259;
-            // ObjDetector.cpp:197) and in-place order-preserving compaction:
-            // kept survivors move to [nn, ...), never past the group just read
-            auto decide = [&](bool valid, unsigned sv, float sum) {
-                bool keep = false;
-                if (valid) {
-                    const float sc = sum / (float)n;
-                    const int li = slot(sv);
-                    st_s[li] = sc;
-                    keep = !((double)sc < (double)th);
-                    st_p[li] = (int8_t)(keep ? s + 1 : s);
-                }
-                const unsigned long long mk = __ballot(keep);
-                wave_sync();
-                if (keep) surv[nn + __popcll(mk & lanes_below())] = sv;
-                nn += __popcll(mk);
-                wave_sync();
-            };
-            if (nsurv >= a.chunk_min || n > kItemBuf) {
-                // one lane per survivor, k wave-uniform: parameters via scalar loads
-                for (int c = 0; c < nsurv; c += 64) {
-                    const int i = c + lane;
-                    unsigned sv = 0;
-                    float sum = 0.0f;
-                    if (i < nsurv) {
-                        sv = surv[i];
-                        const TabView Tj{Tb, cell(sv) << 4};
-                        for (int k = 0; k < n; k++) {
-                            const int gk = off + k;
-                            sum += weak_eval(Tj, half_off, projL[gk], a.w + gk * 9, a.bias[gk]);
-                        }
-                    }
-                    decide(i < nsurv, sv, sum);
-                }
-            } else {
-                // (survivor, weak) items over the lanes, groups of G survivors
-                // whose n*G results fit the wave's LDS buffer.  Items run in
-                // shape-sorted weak order (Ol: few patch shapes per wave
-                // instruction, so little divergence); each survivor's lane then
-                // adds its results in the reference's k order.
-                const int gcap = min(64, kItemBuf / n);
-                for (int c = 0; c < nsurv; c += gcap) {
-                    const int G = min(gcap, nsurv - c), items = G * n;
-                    const float rcp = 1.0f / (float)G;
-                    auto decode = [&](int t2, int &k, int &i) {  // item -> (weak k, survivor i)
-                        int kk = (int)((float)t2 * rcp);                // kk = t2 / G
-                        i = t2 - kk * G;
-                        if (i < 0) { kk--; i += G; }
-                        else if (i >= G) { kk++; i -= G; }
-                        k = Ol[off + kk];
-                    };
-                    for (int t2 = lane; t2 < items; t2 += 64) {
-                        int k, i;
-                        decode(t2, k, i);
-                        const int gk = off + k;
-                        const TabView Tj{Tb, cell(surv[c + i]) << 4};
-                        const ProjPatch pj = load_proj(projL + gk);
-                        P[k * G + i] = LW ? weak_eval(Tj, half_off, pj, Wl + gk * 9, Bl[gk])
-                                          : weak_eval(Tj, half_off, pj, a.w + gk * 9, a.bias[gk]);
-                    }
-                    wave_sync();
-                    unsigned sv = 0;
-                    float acc = 0.0f;  // GentleAdaboost.cpp:255-258 order
-                    if (lane < G) {
-                        sv = surv[c + lane];
-                        for (int k = 0; k < n; k++) acc += P[k * G + lane];
-                    }
-                    decide(lane < G, sv, acc);
+        if (D.nw > 0) {  // (empty strips of narrow rows: nothing to do)
+            const char *Tb = reinterpret_cast<const char *>(a.table + (long long)frame * g.frame4);
+            const WinSet B{(unsigned)D.t_off, D.nw, D.nr, g.step * g.rowp, g.cs,
+                           D.level, D.thr, D.pre_row, D.pre_col};
+            eval_windows<LW>(a, B, Tb, Wl, Bl, Ol, P, st_s, surv, st_p, lane,
+                             [](int) { return true; });
+            // 3) per-window results to HBM (coalesced per row)
+            const long long gi = (long long)frame * a.grid_per_frame + D.g_off;
+            for (int r = 0; r < D.nr; r++) {
+                for (int u = lane; u < D.nw; u += 64) {
+                    a.st_p[gi + (long long)r * D.g_row + u] = st_p[r * D.nw + u];
+                    a.st_s[gi + (long long)r * D.g_row + u] = st_s[r * D.nw + u];
                 }
             }
-            nsurv = nn;
+            wave_sync();
         }
-
-        // 3) per-window results to HBM (coalesced per row)
-        const long long gi = (long long)frame * a.grid_per_frame + D.g_off;
-        for (int r = 0; r < nr; r++) {
-            for (int u = lane; u < nw; u += 64) {
-                a.st_p[gi + (long long)r * D.g_row + u] = st_p[r * nw + u];
-                a.st_s[gi + (long long)r * D.g_row + u] = st_s[r * nw + u];
-            }
-        }
-        wave_sync();
         t = __builtin_amdgcn_readfirstlane(tn);
         if (t < n_tasks) {
             tf = task_index(t);
@@ -366,6 +413,203 @@ __global__ __launch_bounds__(64) void walk_kernel(WalkArgs a) {
     if (lane == 0) a.row_visited[blockIdx.x] = (unsigned)nvis;
 }
 
+constexpr int kBatch = 64;  // chain kernel: windows of one parity evaluated per round
+
+// chain kernel LDS per wave: P f32[kItemBuf] | st_s f32[kBatch] | surv u32[kBatch]
+// | segment scores f32[SEGA] | evaluated, good, detection bits u64[SEGA/64] x 3
+// | st_p i8[kBatch]
+__host__ __device__ inline size_t chain_wave_bytes(int seg_max) {
+    const size_t sa = (size_t)((seg_max + 63) & ~63);
+    return (size_t)kItemBuf * 4 + (size_t)kBatch * 9 + sa * 4 + sa / 64 * 24 + 64;
+}
+
+// Lazy grid (the default detect path).  The reference evaluates only the
+// windows its adaptive-stride x chain visits (ObjDetector.cpp:185-217): after
+// a window with final score < 0.5 (or a prefilter reject) the chain skips one
+// window, after a good one it steps to the next.  Here the chain drives the
+// cascade.  Each row is cut into kXcds segments and XCD x owns segment x of
+// every row (the table columns its L2 sees stay in one band, as in the
+// full-grid kernel).  A task (row, segment) waits for the chain's entry
+// position, published by the task of the segment before it (one 4-B
+// agent-scope word: the payload is the flag), then alternates
+//   - evaluate the next kBatch not-yet-evaluated windows of the chain's
+//     parity (p, p+2, ... up to the segment end): prefilter + cascade,
+//   - advance the chain over evaluated windows (64-bit parity masks, one
+//     step per good window) until it reaches an unevaluated one,
+// and publishes where the chain leaves the segment.  On the C2 frames this
+// evaluates ~55 % of the grid's weak items (the visited windows alone are
+// 53 %).  Visited windows that passed every stage are emitted with score
+// (s + S + 1)/S (:201-212); visited counts are added per row.
+template <bool LW>
+__global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kernel(CascadeArgs a,
+                                                                                  WalkArgs w) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float4 *Wl;
+    double *Bl;
+    int16_t *Ol;
+    stage_model<LW>(a, smem, Wl, Bl, Ol);
+
+    const int sa = (w.row_max + 63) & ~63, nwords = sa >> 6;  // row_max: widest segment
+    unsigned char *ws = smem + model_lds_bytes(a.K, LW) + (size_t)wv * chain_wave_bytes(w.row_max);
+    float *P = reinterpret_cast<float *>(ws);
+    float *st_s = P + kItemBuf;
+    unsigned *surv = reinterpret_cast<unsigned *>(st_s + kBatch);
+    float *s_seg = reinterpret_cast<float *>(surv + kBatch);
+    unsigned long long *evb = reinterpret_cast<unsigned long long *>(s_seg + sa);
+    unsigned long long *gdb = evb + nwords, *dtb = gdb + nwords;
+    int8_t *st_p = reinterpret_cast<int8_t *>(dtb + nwords);
+
+    const TableGeom g = a.g;
+    const int S = a.n_stages, cs = g.cs;
+    const int n_tasks = w.n_rows * a.n_frames;  // per segment queue, in row order
+    int q = (int)xcc_id(), empty = 0;
+    int t = 0;
+    if (lane == 0) t = atomicAdd(&a.queues[q * kQueueStride], 1);
+    t = __builtin_amdgcn_readfirstlane(t);
+    for (;;) {
+        if (t >= n_tasks) {  // this queue is drained: steal from the next XCD's
+            if (++empty == kXcds) break;
+            q = (q + 1) & (kXcds - 1);
+            t = 0;
+            if (lane == 0) t = atomicAdd(&a.queues[q * kQueueStride], 1);
+            t = __builtin_amdgcn_readfirstlane(t);
+            continue;
+        }
+        int tn = 0;  // prefetch the next task index
+        if (lane == 0) tn = atomicAdd(&a.queues[q * kQueueStride], 1);
+        const int frame = t / w.n_rows, row = t - frame * w.n_rows;
+        const int2 rd = w.rows[row];
+        const LevelInfo L = w.levels[rd.x];
+        const int y = rd.y, nx = L.nx, nxs = (nx + kXcds - 1) / kXcds;
+        const int j0 = min(nx, q * nxs), j1 = min(nx, j0 + nxs);  // this segment: [j0, j1)
+        const long long gi0 = (long long)frame * w.grid_per_frame + L.grid_base +
+                              (long long)(y / w.step) * nx;
+        // entry: where the chain enters the segment (j0 or j0 + 1), from segment q - 1
+        int pos = SC_ABL_NOWAIT ? j0 : 0;
+        if (q > 0 && !SC_ABL_NOWAIT) {
+            int e = 0;
+            if (lane == 0) {
+                int *ep = &w.entry[(long long)t * kXcds + q];
+                unsigned spins = 0;  // bounded: a lost hand-off must not hang the GPU
+                while ((e = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins == (1u << 26)) {
+                        atomicAdd(w.err, 1);
+                        e = j0 + 1;
+                        break;
+                    }
+                }
+            }
+            pos = __builtin_amdgcn_readfirstlane(e) - 1;
+        }
+        unsigned nvis = 0;
+        if (pos < j1) {
+            const char *Tb = reinterpret_cast<const char *>(a.table + (long long)frame * g.frame4);
+            const unsigned row_off = (unsigned)(y * g.rowp);
+            const int nseg = j1 - j0;
+            for (int i = lane; i < ((nseg + 63) >> 6); i += 64) {
+                evb[i] = 0ull;
+                gdb[i] = 0ull;
+                dtb[i] = 0ull;
+            }
+            wave_sync();
+            const unsigned long long kEven = 0x5555555555555555ull;
+            int r = pos - j0;  // chain position relative to the segment
+            while (r < nseg) {
+                // evaluate the next kBatch windows of r's parity not yet evaluated
+                const int nb = min(kBatch, (nseg - r + 1) >> 1);
+                const WinSet B{row_off + (unsigned)((j0 + r) * cs), nb, 1, 0, 2 * cs,
+                               rd.x, L.thr, L.pre_row, L.pre_col};
+                auto need = [&](int u) {
+                    const int k = r + 2 * u;
+                    return ((evb[k >> 6] >> (k & 63)) & 1ull) == 0ull;
+                };
+                const bool mine = lane < nb && need(lane);
+                eval_windows<LW>(a, B, Tb, Wl, Bl, Ol, P, st_s, surv, st_p, lane, need);
+                wave_sync();
+                if (mine) {  // merge the batch into the segment's bits
+                    const int k = r + 2 * lane, p = st_p[lane];
+                    const float sc = st_s[lane];
+                    bool good = false;
+                    if (p >= 0) {
+                        const double fin = ((double)sc + p + 1) / S;  // ObjDetector.cpp:201
+                        good = !(fin < w.stride_score);               // :214
+                    }
+                    s_seg[k] = sc;
+                    atomicOr(&evb[k >> 6], 1ull << (k & 63));
+                    if (good) atomicOr(&gdb[k >> 6], 1ull << (k & 63));
+                    if (p == S) atomicOr(&dtb[k >> 6], 1ull << (k & 63));  // passed every stage
+                    if (a.st_p) {  // debug: per-window results for the parity dumps
+                        a.st_p[gi0 + j0 + k] = (int8_t)p;
+                        a.st_s[gi0 + j0 + k] = sc;
+                    }
+                }
+                wave_sync();
+                // advance the chain over evaluated windows: from a landing
+                // position it visits every second window until a good one
+                for (;;) {
+                    const int c = r >> 6, b = r & 63;
+                    const unsigned long long par = (b & 1) ? ~kEven : kEven;
+                    const int lim = min(64, nseg - (c << 6));  // bits past the segment
+                    const unsigned long long inseg = lim == 64 ? ~0ull : ((1ull << lim) - 1ull);
+                    const unsigned long long path = par & (~0ull << b) & inseg;
+                    const unsigned long long ev = evb[c];
+                    const unsigned long long unev = path & ~ev, good = path & ev & gdb[c];
+                    const int f = unev ? __builtin_ctzll(unev) : 64;
+                    const int qg = good ? __builtin_ctzll(good) : 64;
+                    unsigned long long vis;
+                    if (f < qg) {  // an unevaluated window: next batch from there
+                        vis = path & ((1ull << f) - 1ull);
+                        r = (c << 6) + f;
+                    } else if (qg < 64) {  // lands on good window qg, continues at qg + 1
+                        vis = path & (qg == 63 ? ~0ull : ((2ull << qg) - 1ull));
+                        const int k = (c << 6) + qg;
+                        if (lane == 0 && ((dtb[c] >> qg) & 1ull)) {  // detection (:203)
+                            const int slot = atomicAdd(&w.counters[0], 1);
+                            atomicAdd(&w.counters[1 + frame], 1);
+                            if (slot < w.capacity) {
+                                sc_det_record rec;
+                                rec.frame = frame;
+                                rec.level = rd.x;
+                                rec.x = (j0 + k) * w.step;
+                                rec.y = y;
+                                rec.w = L.l;
+                                rec.h = L.lh;
+                                rec.stage_reached = S;
+                                rec._pad = 0;
+                                rec.score = ((double)s_seg[k] + S + 1) / S;  // :201
+                                w.out[slot] = rec;
+                            }
+                        }
+                        r = k + 1;
+                    } else {  // every path bit of this word visited
+                        vis = path;
+                        r = lim < 64 ? nseg + (b & 1) : ((c + 1) << 6) + (b & 1);
+                        if (lim < 64) {  // the chain's next landing past the segment
+                            const int last = 63 - __builtin_clzll(path | 1ull);
+                            r = path ? (c << 6) + last + 2 : r;
+                        }
+                    }
+                    nvis += __popcll(vis);
+                    if (w.dbg_v && ((vis >> lane) & 1ull)) w.dbg_v[gi0 + j0 + (c << 6) + lane] = 1;
+                    if (f < qg || r >= nseg) break;
+                }
+            }
+            pos = j0 + r;
+        }
+        // hand the chain to the next segment (one agent-scope word: value + 1)
+        if (lane == 0) {
+            if (q + 1 < kXcds)
+                __hip_atomic_store(&w.entry[(long long)t * kXcds + q + 1], pos + 1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (nvis) atomicAdd(&w.row_visited[t], nvis);
+        }
+        wave_sync();
+        t = __builtin_amdgcn_readfirstlane(tn);
+    }
+}
+
 }  // namespace
 
 int launch_cascade(const CascadeArgs &a, int device, hipStream_t s) {
@@ -399,6 +643,36 @@ int launch_cascade(const CascadeArgs &a, int device, hipStream_t s) {
 
 void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s) {
     hipLaunchKernelGGL(walk_kernel, dim3(a.n_rows * n_frames), dim3(64), 0, s, a);
+}
+
+int launch_chain(const CascadeArgs &a, const WalkArgs &w, int device, hipStream_t s) {
+    const size_t scratch = kWavesPerWg * chain_wave_bytes(w.row_max);
+    bool lw = model_lds_bytes(a.K, true) + scratch <= 160 * 1024;
+    if (const char *e = std::getenv("SC_LDS_WEIGHTS")) lw = std::atoi(e) != 0;  // tuning override
+    const size_t lds = model_lds_bytes(a.K, lw) + scratch;
+    static int cus = 0, dev_cached = -1;
+    if (dev_cached != device) {
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        dev_cached = device;
+    }
+    int per_cu = 0;
+    if (lw)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<true>, kCascadeThreads, lds);
+    else
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<false>, kCascadeThreads, lds);
+    per_cu = std::max(1, std::min(per_cu, 4));
+    if (const char *e = std::getenv("SC_WGS_PER_CU"))  // tuning override
+        per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
+    const int grid = std::max(1, cus) * per_cu;
+    if (lw)
+        hipLaunchKernelGGL(chain_kernel<true>, dim3(grid), dim3(kCascadeThreads), lds, s, a, w);
+    else
+        hipLaunchKernelGGL(chain_kernel<false>, dim3(grid), dim3(kCascadeThreads), lds, s, a, w);
+    return grid;
+}
+
+size_t chain_lds_bytes(int K, int row_max) {  // smallest variant
+    return model_lds_bytes(K, false) + kWavesPerWg * chain_wave_bytes(row_max);
 }
 
 size_t cascade_lds_bytes(int K, int strip_max, int band_rows) {  // smallest variant

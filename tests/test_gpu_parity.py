@@ -50,12 +50,16 @@ def _grid_parity(sc, oracle, cascade, cfg, img, params_sc, params_or):
     T = oracle.integral(img)
     rp, rs = oracle.eval_grid(T, cascade, params_or)
     assert len(p) == len(rp)
-    np.testing.assert_array_equal(p, rp)
-    assert s.view(np.uint32).tobytes() == rs.view(np.uint32).tobytes()
+    # lazy grid (default): only windows the x chain reaches are evaluated (-2
+    # elsewhere); SC_FULL_GRID=1 evaluates all of them
+    ev = p != -2
+    np.testing.assert_array_equal(p[ev], rp[ev])
+    assert s[ev].view(np.uint32).tobytes() == rs[ev].view(np.uint32).tobytes()
     H, W = img.shape
     layout, _ = oracle.grid_layout(W, H, params_or)
     rv, rdm = oracle.walk_rows(rp, rs, layout, cascade.n_stages, params_or.stride_score)
     np.testing.assert_array_equal(v, rv)
+    assert ev[rv.astype(bool)].all()  # every visited window was evaluated
     ref, nvis = oracle.detect(T, cascade, params_or)
     assert det.info("visited") == nvis == int(rv.sum())
     assert _det_set(wins) == _det_set(ref)
@@ -68,7 +72,10 @@ def test_grid_parity_640x480_single_scale(sc, oracle, face_cascade):
                  oracle.Params(n_levels=1))
 
 
-def test_grid_parity_1080p_24_levels(sc, oracle, face_cascade):
+@pytest.mark.parametrize("full", [None, "1"])
+def test_grid_parity_1080p_24_levels(sc, oracle, face_cascade, monkeypatch, full):
+    if full:
+        monkeypatch.setenv("SC_FULL_GRID", full)
     img = _frame(1920, 1080, 1000)
     _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=24),
                  oracle.Params(n_levels=24))
@@ -79,16 +86,17 @@ def test_grid_parity_default_levels_odd_size(sc, oracle, face_cascade):
     _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(), oracle.Params())
 
 
-@pytest.mark.parametrize("chunk_min,substrips,band_rows,layout", [
-    ("1", None, None, None), ("40", None, "3", "0"), (None, "3", "1", "1"), (None, "2", "5", None),
-    ("1", None, "2", "1"), (None, None, None, "0"), (None, None, None, "1")])
+@pytest.mark.parametrize("chunk_min,substrips,band_rows,layout,full", [
+    ("1", None, None, None, "1"), ("40", None, "3", "0", "1"), (None, "3", "1", "1", "1"),
+    (None, "2", "5", None, "1"), ("1", None, "2", "1", "1"), (None, None, None, "0", None),
+    (None, None, None, "1", None), ("1", None, None, None, None), (None, None, None, None, "1")])
 def test_grid_parity_kernel_paths(sc, oracle, face_cascade, monkeypatch, chunk_min, substrips,
-                                  band_rows, layout):
+                                  band_rows, layout, full):
     """The one-lane-per-window stage path (used for stages with more weak
     classifiers than the item buffer holds), other strip splits, band heights
     and both table cell formats give the same bits as the defaults."""
     for k, v in (("SC_CHUNK_MIN", chunk_min), ("SC_SUBSTRIPS", substrips),
-                 ("SC_BAND_ROWS", band_rows), ("SC_TABLE_LAYOUT", layout)):
+                 ("SC_BAND_ROWS", band_rows), ("SC_TABLE_LAYOUT", layout), ("SC_FULL_GRID", full)):
         if v:
             monkeypatch.setenv(k, v)
     img = _frame(1280, 720, 77)
@@ -111,8 +119,11 @@ def test_pedestrian_64x128(sc, oracle, ped_cascade, monkeypatch, lds_weights):
                  oracle.Params(base_len=64, aspect_h=2, n_levels=12))
 
 
-def test_permissive_cascade_many_detections(sc, oracle, face_cascade):
+@pytest.mark.parametrize("full", [None, "1"])
+def test_permissive_cascade_many_detections(sc, oracle, face_cascade, monkeypatch, full):
     """Lowered thetas: many windows reach the last stage (detections + stride 1)."""
+    if full:
+        monkeypatch.setenv("SC_FULL_GRID", full)
     from surfcascade_amd import synth
     c = face_cascade
     theta = np.full(c.n_stages, 0.2, np.float32)
@@ -149,7 +160,9 @@ def test_constant_image_no_windows(sc):
     det.set_debug(True)
     assert len(det.detect(img)) == 0
     p, s, v = det.dump_grid()
-    assert (p == -1).all()
+    ev = p != -2  # lazy grid: with every window rejected the chain stays on one parity
+    assert (p[ev] == -1).all()
+    assert (ev == v.astype(bool)).all()
     # every row walked at stride 2*step: visited = ceil(nx/2) per row
     assert det.info("visited") == int(v.sum())
 
