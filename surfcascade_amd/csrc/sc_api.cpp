@@ -120,6 +120,7 @@ struct sc_detector {
     DevBuf<unsigned> d_visited;  // per (frame, row): windows the x chain visited
     DevBuf<int> d_queues;       // per-XCD task counters of the cascade kernel
     DevBuf<int> d_entry;        // chain kernel: per (row, segment) chain entry + 1
+    long long err_word = -1;    // chain kernel: index of the hand-off watchdog word in d_entry
     DevBuf<int8_t> d_st_p;      // per grid window: stage reached (-1 prefilter reject)
     DevBuf<float> d_st_s;       // per grid window: last stage score
     // debug
@@ -199,20 +200,27 @@ void build_geometry(sc_detector *d, int W, int H) {
         t.W = W;
         t.H = H;
         t.step = ng.step;
-        const int Q = (W + 1 + ng.step - 1) / ng.step;
+        // parity-split phase planes: the lazy grid's batches (one parity,
+        // windows 2 apart) then read consecutive cells
+        const char *ep = std::getenv("SC_PHASES");  // tuning override: 1 = step planes
+        t.ph = (ep && std::atoi(ep) == 1) ? ng.step : 2 * ng.step;
+        const int Q = (W + 1 + t.ph - 1) / t.ph;
         t.Qp = (Q + 15) & ~15;
-        t.rowp = 2 * ng.step * t.Qp;
+        t.rowp = 2 * t.ph * t.Qp;
         const char *el = std::getenv("SC_TABLE_LAYOUT");  // tuning override
         const bool split = el ? std::atoi(el) == 0 : kSplitLayout;
         t.cs = split ? 1 : 2;
-        t.hs = split ? ng.step * t.Qp : 1;
+        t.hs = split ? t.ph * t.Qp : 1;
         t.frame4 = (long long)(H + 1) * t.rowp;
         if ((long long)(H + 1) * t.rowp > (1ll << 28))  // byte offsets within a frame table: u32
             throw Error{SC_ERR_INVALID, "frame too large for 32-bit table offsets"};
     }
     const sc::TableGeom &tg = ng.tg;
-    auto col_off = [&](int cx) { return tg.at(cx, 0); };
-    ng.proj.resize((size_t)ng.n_levels * d->K);
+    // cell of column cx relative to the window origin, for windows of parity
+    // par (x = step*j, j % 2 == par): at(x + cx) - at(x) depends on x only
+    // through that parity
+    auto col_off = [&](int par, int cx) { return tg.at(ng.step * par + cx, 0) - tg.at(ng.step * par, 0); };
+    ng.proj.resize((size_t)ng.n_levels * 2 * d->K);
     long long gb = 0;
     for (int i = 0; i < ng.n_levels; i++) {
         sc::LevelInfo L{};
@@ -223,7 +231,8 @@ void build_geometry(sc_detector *d, int W, int H) {
         if (L.l >= 1 && L.l <= W && L.lh <= H) {
             L.nx = (W - L.l) / ng.step + 1;
             L.ny = (H - L.lh) / ng.step + 1;
-            L.pre_col = col_off(L.l);
+            L.pre_col[0] = col_off(0, L.l);
+            L.pre_col[1] = col_off(1, L.l);
             L.pre_row = L.lh * tg.rowp;
             if (L.nx > 4096)  // walk kernel: one wave, 64 chunks of 64 windows per row
                 throw Error{SC_ERR_INVALID, "more than 4096 windows per row (frame too wide)"};
@@ -234,7 +243,7 @@ void build_geometry(sc_detector *d, int W, int H) {
         // ProjectPatches (DenseSURFFeatureExtractor.cpp:459-484) + cell split
         // (GetRectsFromPatch :360-377) for every fitted patch at this level.
         const float scale = (float)L.l / (float)p.tmpl_w;
-        auto project = [&](const int32_t *r) {
+        auto project = [&](const int32_t *r, int par) {
             int px = (int)((float)r[0] * scale), py = (int)((float)r[1] * scale), pw, ph;
             if (r[2] >= r[3]) {
                 int ratio = r[2] / r[3];
@@ -264,13 +273,16 @@ void build_geometry(sc_detector *d, int W, int H) {
                                                 std::to_string(i)};
             pp.row0 = py * tg.rowp;
             pp.rowstep = c * tg.rowp;
-            for (int q = 0; q <= gw; q++) pp.col[q] = col_off(px + q * c);
+            for (int q = 0; q <= gw; q++) pp.col[q] = col_off(par, px + q * c);
             return pp;
         };
-        for (int k = 0; k < d->K; k++) ng.proj[(size_t)i * d->K + k] = project(&d->patch_rects[4 * k]);
-        if (d->miner)  // ExtractFeatures over every template patch (:88-93)
-            for (size_t j = 0; j < d->all_rects.size() / 4; j++)
-                ng.proj_all.push_back(project(&d->all_rects[4 * j]));
+        for (int par = 0; par < 2; par++) {
+            for (int k = 0; k < d->K; k++)
+                ng.proj[((size_t)i * 2 + par) * d->K + k] = project(&d->patch_rects[4 * k], par);
+            if (d->miner)  // ExtractFeatures over every template patch (:88-93)
+                for (size_t j = 0; j < d->all_rects.size() / 4; j++)
+                    ng.proj_all.push_back(project(&d->all_rects[4 * j], par));
+        }
         ng.levels.push_back(L);
     }
     ng.grid = gb;  // may be 0: no window fits (the reference loop runs 0 times)
@@ -303,12 +315,14 @@ void build_geometry(sc_detector *d, int W, int H) {
                 t.nw = std::max(0, std::min(L.nx, j0 + nxs) - j0);
                 t.nr = (int)(r1 - r0);
                 t.g_row = L.nx;
-                t.t_off = y * tg.rowp + j0 * tg.cs;
+                t.t_off = y * tg.rowp;
+                t.j0 = j0;
                 t.g_off = (int)(L.grid_base + (long long)(y / ng.step) * L.nx + j0);
                 t.level = lv;
                 t.thr = L.thr;
                 t.pre_row = L.pre_row;
-                t.pre_col = L.pre_col;
+                t.pre_col[0] = L.pre_col[0];
+                t.pre_col[1] = L.pre_col[1];
                 ng.tasks.push_back(t);
             }
             r0 = r1;
@@ -538,24 +552,39 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     wk.row_visited = d->d_visited.p;
     wk.dbg_v = d->debug ? d->d_dbg_v.p : nullptr;
     wk.row_max = seg_max;
-    if (lazy) {  // the walk drives the cascade: one chain kernel
-        const size_t n_tasks = g.rows.size() * (size_t)n;
-        d->d_entry.ensure(n_tasks * sc::kXcds + 1);
-        wk.entry = d->d_entry.p;
-        wk.err = d->d_entry.p + n_tasks * sc::kXcds;  // zeroed with the entries
-        HIPCHK(hipMemsetAsync(d->d_entry.p, 0, sizeof(int) * (n_tasks * sc::kXcds + 1), d->stream));
-        HIPCHK(hipMemsetAsync(d->d_visited.p, 0, sizeof(unsigned) * n_tasks, d->stream));
+    if (lazy) {  // the walk drives the cascade: one chain kernel per chunk of frames
+        const size_t n_rows = g.rows.size();
+        // table offsets are 32-bit byte offsets from the chunk's first frame
+        const int chunk = (int)std::max<long long>(1, (1ll << 28) / g.tg.frame4);
+        d->d_entry.ensure(n_rows * std::min(chunk, n) * sc::kXcds + 1);
         if (d->debug) {  // dumps: unevaluated windows read -2, unvisited 0
             HIPCHK(hipMemsetAsync(d->d_st_p.p, 0xFE, (size_t)g.grid * n, d->stream));
             HIPCHK(hipMemsetAsync(d->d_st_s.p, 0, sizeof(float) * (size_t)g.grid * n, d->stream));
             HIPCHK(hipMemsetAsync(d->d_dbg_v.p, 0, (size_t)g.grid * n, d->stream));
-        } else {
-            ca.st_p = nullptr;
-            ca.st_s = nullptr;
         }
+        HIPCHK(hipMemsetAsync(d->d_visited.p, 0, sizeof(unsigned) * n_rows * n, d->stream));
         timed_begin(d, &e0);
-        sc::launch_chain(ca, wk, d->device, d->stream);
-        HIPCHK(hipGetLastError());
+        for (int f0 = 0; f0 < n; f0 += chunk) {
+            const int nc = std::min(chunk, n - f0);
+            sc::CascadeArgs cc = ca;
+            sc::WalkArgs wc = wk;
+            cc.table = d->d_table.p + (size_t)f0 * g.tg.frame4;
+            cc.n_frames = nc;
+            cc.st_p = d->debug ? d->d_st_p.p + (size_t)f0 * g.grid : nullptr;
+            cc.st_s = d->debug ? d->d_st_s.p + (size_t)f0 * g.grid : nullptr;
+            wc.dbg_v = d->debug ? d->d_dbg_v.p + (size_t)f0 * g.grid : nullptr;
+            wc.row_visited = d->d_visited.p + (size_t)f0 * n_rows;
+            wc.entry = d->d_entry.p;
+            d->err_word = (long long)(n_rows * std::min(chunk, n) * sc::kXcds);
+            wc.err = d->d_entry.p + d->err_word;
+            wc.frame0 = f0;
+            HIPCHK(hipMemsetAsync(d->d_entry.p, 0, sizeof(int) * (n_rows * nc * sc::kXcds + 1) , d->stream));
+            if (f0 > 0)
+                HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kXcds * sc::kQueueStride,
+                                      d->stream));
+            sc::launch_chain(cc, wc, d->device, d->stream);
+            HIPCHK(hipGetLastError());
+        }
         timed_end(d, SC_KERNEL_WINDOWS, e0);
         return;
     }
@@ -567,11 +596,9 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
 
 // The chain kernel's hand-off watchdog (reads after the stream has drained).
 void check_chain(sc_detector *d) {
-    if (!d->lazy || d->d_entry.n == 0) return;
-    const size_t n_tasks = d->geo.rows.size() * (size_t)d->last_frames;
-    if (d->d_entry.n < n_tasks * sc::kXcds + 1) return;
+    if (!d->lazy || d->err_word < 0) return;
     int err = 0;
-    HIPCHK(hipMemcpy(&err, d->d_entry.p + n_tasks * sc::kXcds, sizeof(int), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&err, d->d_entry.p + d->err_word, sizeof(int), hipMemcpyDeviceToHost));
     if (err) throw Error{SC_ERR_DEVICE, "chain kernel: " + std::to_string(err) + " segment hand-off(s) timed out"};
 }
 

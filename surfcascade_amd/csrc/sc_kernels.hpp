@@ -28,14 +28,20 @@ constexpr int kQueueStride = 64;  // ints between per-XCD queue words (own 256-B
 
 struct TableGeom {
     int W, H, step;
-    int Qp;    // cells per phase plane (>= ceil((W+1)/step), multiple of 16)
-    int rowp;  // float4 per table row = 2*step*Qp
+    int ph;    // phase planes per row half: step, or 2*step (windows of one parity adjacent)
+    int Qp;    // cells per phase plane (>= ceil((W+1)/ph), multiple of 16)
+    int rowp;  // float4 per table row = 2*ph*Qp
     int cs;    // float4 per cell step: 1 (channel-split halves) or 2 (8 channels together)
-    int hs;    // float4 from a cell's channels 0-3 to its channels 4-7: step*Qp or 1
+    int hs;    // float4 from a cell's channels 0-3 to its channels 4-7: ph*Qp or 1
     long long frame4;  // float4 per frame table = (H+1)*rowp
     // float4 index of (x, half) within a table row
     __host__ __device__ int at(int x, int h) const {
-        return cs * ((x % step) * Qp + x / step) + h * hs;
+        return cs * ((x % ph) * Qp + x / ph) + h * hs;
+    }
+    // origin cell of grid window j (x = step*j) within its table row: windows
+    // of one parity sit in consecutive cells when ph = 2*step
+    __host__ __device__ int win_cell(int j) const {
+        return ph == step ? cs * j : cs * ((j & 1) * step * Qp + (j >> 1));
     }
 };
 
@@ -45,9 +51,9 @@ struct LevelInfo {
     int nx, ny;           // grid windows per row / rows
     long long grid_base;  // first grid index of the level (canonical order)
     float thr;            // (float)(l*lh) * prefilter_k   (ObjDetector.cpp:188)
-    int pre_col;          // cell offset of column x+l: (l%step)*Qp + l/step
+    int pre_col[2];       // cell of column x+l relative to x, by window parity
     int pre_row;          // lh*rowp
-    int pad[3];
+    int pad[2];
 };
 
 // A fitted patch projected to one level (ProjectPatches + GetRectsFromPatch,
@@ -78,23 +84,24 @@ struct RowScanArgs {
 // others when empty), so the rows its L2 sees stay in a narrow column band.
 // One strip of one band, precomputed on the host (one load per task).
 struct TaskDesc {
-    int t_off;    // table offset (float4) of the strip's first window: y*rowp + j0
-    int g_off;    // grid index (within a frame) of that window
+    int t_off;    // table offset (float4) of the band's first row: y*rowp
+    int g_off;    // grid index (within a frame) of the strip's first window
     int nw;       // windows per row of the strip (0: empty strip)
     int nr;       // grid rows in the band
     int g_row;    // grid index distance between the band's rows (= level nx)
     int level;
     float thr;    // prefilter threshold (float)(l*lh)*k   (ObjDetector.cpp:188)
     int pre_row;  // lh*rowp
-    int pre_col;  // (l%step)*Qp + l/step
-    int pad[3];
+    int pre_col[2];  // LevelInfo::pre_col
+    int j0;       // the strip's first window in its row
+    int pad;
 };
 
 struct CascadeArgs {
     const float4 *table;
     TableGeom g;
     const TaskDesc *tasks;  // [n_bands][kXcds*n_sub]
-    const ProjPatch *proj;  // [n_levels][K]
+    const ProjPatch *proj;  // [n_levels][2 parities][K]
     const float4 *w;        // [K][9]: w[0..32] + 3 pad
     const double *bias;     // [K]
     const float *theta;     // [S]
@@ -129,6 +136,7 @@ struct WalkArgs {
     int row_max;     // chain kernel: most windows in one row segment (LDS sizing)
     int *entry;      // chain kernel: [frame*rows][kXcds] chain entry + 1 per segment (zeroed)
     int *err;        // chain kernel: hand-off timeouts (must stay 0)
+    int frame0;      // chain kernel: first frame of this launch (record frame index)
 };
 
 // Hard-negative mining (sc_mine.hip, FillNegSamples): candidate selection
@@ -157,7 +165,7 @@ struct FeatureArgs {
     TableGeom g;
     const MineWindow *windows;
     int n_windows, n_patches;
-    const ProjPatch *proj_all;  // [n_levels][n_patches]: every template patch projected
+    const ProjPatch *proj_all;  // [n_levels][2 parities][n_patches]: every template patch
     float *out;                 // [n_windows][n_patches][32]
 };
 

@@ -88,7 +88,8 @@ __global__ __launch_bounds__(256) void features_kernel(FeatureArgs a) {
     if (t >= (long long)a.n_windows * a.n_patches) return;
     const int i = (int)(t / a.n_patches), j = (int)(t - (long long)i * a.n_patches);
     const MineWindow w = a.windows[i];
-    const ProjPatch pj = load_proj(a.proj_all + (long long)w.level * a.n_patches + j);
+    const int par = (w.x / a.g.step) & 1;
+    const ProjPatch pj = load_proj(a.proj_all + ((long long)w.level * 2 + par) * a.n_patches + j);
     const TabView T{reinterpret_cast<const char *>(a.table),
                     (unsigned)(w.y * a.g.rowp + a.g.at(w.x, 0)) << 4};
     float f[32];

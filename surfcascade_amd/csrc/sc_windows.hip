@@ -92,12 +92,49 @@ __host__ __device__ inline size_t model_lds_bytes(int K, bool LW) {
 
 // A set of windows of one level: nr rows of nw windows; window (r, u) has
 // its origin cell (phase 0, half 0) at t_off + r*row_cells + u*wstep.
-struct WinSet {
-    unsigned t_off;
-    int nw, nr, row_cells, wstep;
-    int level;
+// Row-set policies of eval_windows.  A survivor is (r << 16 | u): window u
+// of row r; its LDS slot r*stride() + u.
+struct BandRows {  // full grid: nr rows of one level, windows j0 + u of row r
+    unsigned t_off;   // row 0's table row
+    int nw, nr, row_cells, j0, K;
     float thr;  // prefilter threshold (ObjDetector.cpp:188)
+    int pre_row, pre_col0, pre_col1;
+    const ProjPatch *projL;  // the level's projected fitted patches [2 parities][K]
+    TableGeom g;
+    __device__ int rows() const { return nr; }
+    __device__ int stride() const { return nw; }
+    __device__ int width(int) const { return nw; }
+    __device__ unsigned origin(int r, int u) const {
+        return t_off + r * row_cells + g.win_cell(j0 + u);
+    }
+    __device__ float thr_of(int) const { return thr; }
+    __device__ int pre_row_of(int) const { return pre_row; }
+    __device__ int pre_col_of(int, int u) const { return ((j0 + u) & 1) ? pre_col1 : pre_col0; }
+    __device__ const ProjPatch *proj_of(int, int u) const { return projL + ((j0 + u) & 1) * K; }
+};
+
+// chain kernel: one row per task slot, each with its own frame, level and
+// chain position; descriptors in LDS (t_off counts from frame 0's table)
+struct SlotDesc {
+    unsigned t_off;  // origin cell of the slot's first batch window
+    int nw;          // windows in the batch (0: slot idle), all of one parity
+    float thr;
     int pre_row, pre_col;
+    int proj;        // (level * 2 + parity) * K
+    int pad[2];
+};
+struct SlotRows {
+    const SlotDesc *d;
+    int nr, bstride, wstep;
+    const ProjPatch *proj;
+    __device__ int rows() const { return nr; }
+    __device__ int stride() const { return bstride; }
+    __device__ int width(int r) const { return d[r].nw; }
+    __device__ unsigned origin(int r, int u) const { return d[r].t_off + u * wstep; }
+    __device__ float thr_of(int r) const { return d[r].thr; }
+    __device__ int pre_row_of(int r) const { return d[r].pre_row; }
+    __device__ int pre_col_of(int r, int) const { return d[r].pre_col; }
+    __device__ const ProjPatch *proj_of(int r, int) const { return proj + d[r].proj; }
 };
 
 // The per-window work of the detect loop for the windows `need(slot)`
@@ -110,33 +147,32 @@ struct WinSet {
 //      lanes in shape-sorted weak order, results through LDS, each survivor's
 //      lane adds them in the model's k order (GentleAdaboost.cpp:255-258);
 //      the theta test (:197) and order-preserving compaction.
-template <bool LW, class Need>
-__device__ __forceinline__ void eval_windows(const CascadeArgs &a, const WinSet &B, const char *Tb,
+template <bool LW, class Rows, class Need>
+__device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B, const char *Tb,
                                              const float4 *Wl, const double *Bl, const int16_t *Ol,
                                              float *P, float *st_s, unsigned *surv, int8_t *st_p,
                                              int lane, Need need) {
-    const int K = a.K, half_off = a.g.hs;
-    const int nw = B.nw;
-    const float4 *T = reinterpret_cast<const float4 *>(Tb) + B.t_off;
-    // a survivor is (r << 16 | u); its LDS slot r*nw + u
-    auto cell = [&](unsigned sv) {
-        return B.t_off + (sv >> 16) * B.row_cells + (sv & 0xffffu) * B.wstep;
-    };
-    auto slot = [&](unsigned sv) { return (int)(sv >> 16) * nw + (int)(sv & 0xffffu); };
+    const int half_off = a.g.hs, stride = B.stride();
+    const float4 *T = reinterpret_cast<const float4 *>(Tb);
+    auto cell = [&](unsigned sv) { return B.origin((int)(sv >> 16), (int)(sv & 0xffffu)); };
+    auto slot = [&](unsigned sv) { return (int)(sv >> 16) * stride + (int)(sv & 0xffffu); };
 
     // 1) prefilter; survivors in (row, x) order
     int nsurv = 0;
-    for (int r = 0; r < B.nr; r++) {
+    for (int r = 0; r < B.rows(); r++) {
+        const int nw = B.width(r), pre_row = B.pre_row_of(r);
+        const float thr = B.thr_of(r);
         for (int b = 0; b < nw; b += 64) {
             const int u = b + lane;
             bool pass = false;
-            if (u < nw && need(r * nw + u)) {
-                const float4 *t0 = T + r * B.row_cells + u * B.wstep;
-                const float4 v = box4(t0[0], t0[B.pre_row + B.pre_col], t0[B.pre_col], t0[B.pre_row]);
+            if (u < nw && need(r * stride + u)) {
+                const int pre_col = B.pre_col_of(r, u);
+                const float4 *t0 = T + B.origin(r, u);
+                const float4 v = box4(t0[0], t0[pre_row + pre_col], t0[pre_col], t0[pre_row]);
                 const float m = (((v.x + v.y) + v.z) + v.w) / 2.0f;  // sum(), :351-358
-                pass = m > B.thr;                                    // ObjDetector.cpp:188
-                st_p[r * nw + u] = pass ? 0 : -1;
-                st_s[r * nw + u] = 0.0f;
+                pass = m > thr;                                      // ObjDetector.cpp:188
+                st_p[r * stride + u] = pass ? 0 : -1;
+                st_s[r * stride + u] = 0.0f;
             }
             const unsigned long long mk = __ballot(pass);
             if (pass) surv[nsurv + __popcll(mk & lanes_below())] = ((unsigned)r << 16) | (unsigned)u;
@@ -146,7 +182,6 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const WinSet 
     wave_sync();
 
     // 2) cascade, stage by stage over the compacted survivors
-    const ProjPatch *projL = a.proj + (long long)B.level * K;
     for (int s = 0; s < a.n_stages && nsurv > 0; s++) {
         const int off = a.stage_off[s], n = a.stage_off[s + 1] - off;
         const float th = a.theta[s];
@@ -178,6 +213,7 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const WinSet 
                 if (i < nsurv) {
                     sv = surv[i];
                     const TabView Tj{Tb, cell(sv) << 4};
+                    const ProjPatch *projL = B.proj_of((int)(sv >> 16), (int)(sv & 0xffffu));
                     for (int k = 0; k < n; k++) {
                         const int gk = off + k;
                         sum += weak_eval(Tj, half_off, projL[gk], a.w + gk * 9, a.bias[gk]);
@@ -206,8 +242,9 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const WinSet 
                     int k, i;
                     decode(t2, k, i);
                     const int gk = off + k;
-                    const TabView Tj{Tb, cell(surv[c + i]) << 4};
-                    const ProjPatch pj = load_proj(projL + gk);
+                    const unsigned sv = surv[c + i];
+                    const TabView Tj{Tb, cell(sv) << 4};
+                    const ProjPatch pj = load_proj(B.proj_of((int)(sv >> 16), (int)(sv & 0xffffu)) + gk);
                     P[k * G + i] = LW ? weak_eval(Tj, half_off, pj, Wl + gk * 9, Bl[gk])
                                       : weak_eval(Tj, half_off, pj, a.w + gk * 9, a.bias[gk]);
                 }
@@ -302,8 +339,9 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
         const int frame = tf.y;
         if (D.nw > 0) {  // (empty strips of narrow rows: nothing to do)
             const char *Tb = reinterpret_cast<const char *>(a.table + (long long)frame * g.frame4);
-            const WinSet B{(unsigned)D.t_off, D.nw, D.nr, g.step * g.rowp, g.cs,
-                           D.level, D.thr, D.pre_row, D.pre_col};
+            const BandRows B{(unsigned)D.t_off, D.nw, D.nr, g.step * g.rowp, D.j0, a.K, D.thr,
+                             D.pre_row, D.pre_col[0], D.pre_col[1],
+                             a.proj + (long long)D.level * 2 * a.K, g};
             eval_windows<LW>(a, B, Tb, Wl, Bl, Ol, P, st_s, surv, st_p, lane,
                              [](int) { return true; });
             // 3) per-window results to HBM (coalesced per row)
@@ -413,14 +451,19 @@ __global__ __launch_bounds__(64) void walk_kernel(WalkArgs a) {
     if (lane == 0) a.row_visited[blockIdx.x] = (unsigned)nvis;
 }
 
-constexpr int kBatch = 64;  // chain kernel: windows of one parity evaluated per round
+#ifndef SC_CHAIN_SLOTS  // chain kernel: rows (tasks) a wave advances together
+#define SC_CHAIN_SLOTS 2
+#endif
+constexpr int kSlots = SC_CHAIN_SLOTS;
+constexpr int kBatch = 64;  // chain kernel: windows of one parity per slot and round
 
-// chain kernel LDS per wave: P f32[kItemBuf] | st_s f32[kBatch] | surv u32[kBatch]
-// | segment scores f32[SEGA] | evaluated, good, detection bits u64[SEGA/64] x 3
-// | st_p i8[kBatch]
+// chain kernel LDS per wave: P f32[kItemBuf] | st_s f32[kSlots*kBatch] |
+// surv u32[kSlots*kBatch] | per slot: segment scores f32[SEGA], evaluated /
+// good / detection bits u64[SEGA/64] x 3 | SlotDesc[kSlots] | st_p i8[kSlots*kBatch]
 __host__ __device__ inline size_t chain_wave_bytes(int seg_max) {
     const size_t sa = (size_t)((seg_max + 63) & ~63);
-    return (size_t)kItemBuf * 4 + (size_t)kBatch * 9 + sa * 4 + sa / 64 * 24 + 64;
+    return (size_t)kItemBuf * 4 + (size_t)kSlots * kBatch * 9 +
+           (size_t)kSlots * (sa * 4 + sa / 64 * 24) + kSlots * sizeof(SlotDesc) + 64;
 }
 
 // Lazy grid (the default detect path).  The reference evaluates only the
@@ -429,17 +472,19 @@ __host__ __device__ inline size_t chain_wave_bytes(int seg_max) {
 // window, after a good one it steps to the next.  Here the chain drives the
 // cascade.  Each row is cut into kXcds segments and XCD x owns segment x of
 // every row (the table columns its L2 sees stay in one band, as in the
-// full-grid kernel).  A task (row, segment) waits for the chain's entry
-// position, published by the task of the segment before it (one 4-B
+// full-grid kernel).  A task (row, segment) starts from the chain's entry
+// position, published by the task of the previous segment (one 4-B
 // agent-scope word: the payload is the flag), then alternates
 //   - evaluate the next kBatch not-yet-evaluated windows of the chain's
 //     parity (p, p+2, ... up to the segment end): prefilter + cascade,
 //   - advance the chain over evaluated windows (64-bit parity masks, one
 //     step per good window) until it reaches an unevaluated one,
-// and publishes where the chain leaves the segment.  On the C2 frames this
-// evaluates ~55 % of the grid's weak items (the visited windows alone are
-// 53 %).  Visited windows that passed every stage are emitted with score
-// (s + S + 1)/S (:201-212); visited counts are added per row.
+// and publishes where the chain leaves the segment.  A wave carries kSlots
+// tasks at once and evaluates their batches together (one prefilter pass,
+// one set of stage rounds), so the stage-by-stage round trips serve twice
+// the windows.  On the C2 frames the lazy grid evaluates ~55 % of the grid's
+// weak items (the visited windows alone are 53 %).  Visited windows that
+// passed every stage are emitted with score (s + S + 1)/S (:201-212).
 template <bool LW>
 __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kernel(CascadeArgs a,
                                                                                   WalkArgs w) {
@@ -454,159 +499,237 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
     unsigned char *ws = smem + model_lds_bytes(a.K, LW) + (size_t)wv * chain_wave_bytes(w.row_max);
     float *P = reinterpret_cast<float *>(ws);
     float *st_s = P + kItemBuf;
-    unsigned *surv = reinterpret_cast<unsigned *>(st_s + kBatch);
-    float *s_seg = reinterpret_cast<float *>(surv + kBatch);
-    unsigned long long *evb = reinterpret_cast<unsigned long long *>(s_seg + sa);
-    unsigned long long *gdb = evb + nwords, *dtb = gdb + nwords;
-    int8_t *st_p = reinterpret_cast<int8_t *>(dtb + nwords);
+    unsigned *surv = reinterpret_cast<unsigned *>(st_s + kSlots * kBatch);
+    float *s_seg0 = reinterpret_cast<float *>(surv + kSlots * kBatch);
+    unsigned long long *bits0 = reinterpret_cast<unsigned long long *>(s_seg0 + kSlots * sa);
+    SlotDesc *desc = reinterpret_cast<SlotDesc *>(bits0 + kSlots * 3 * nwords);
+    int8_t *st_p = reinterpret_cast<int8_t *>(desc + kSlots);
+    auto s_seg = [&](int sl) { return s_seg0 + sl * sa; };
+    auto evb = [&](int sl) { return bits0 + (sl * 3 + 0) * nwords; };
+    auto gdb = [&](int sl) { return bits0 + (sl * 3 + 1) * nwords; };
+    auto dtb = [&](int sl) { return bits0 + (sl * 3 + 2) * nwords; };
 
     const TableGeom g = a.g;
     const int S = a.n_stages, cs = g.cs;
     const int n_tasks = w.n_rows * a.n_frames;  // per segment queue, in row order
+    const unsigned long long kEven = 0x5555555555555555ull;
     int q = (int)xcc_id(), empty = 0;
-    int t = 0;
-    if (lane == 0) t = atomicAdd(&a.queues[q * kQueueStride], 1);
-    t = __builtin_amdgcn_readfirstlane(t);
+    bool drained = false;
+    unsigned idle = 0;  // rounds with every task waiting for its entry
+
+    // per-slot task state (wave-uniform)
+    int st[kSlots], tq[kSlots], tt[kSlots], r[kSlots], j0[kSlots], nseg[kSlots];
+    int frame[kSlots], level[kSlots];
+    unsigned nvis[kSlots];
+#pragma unroll
+    for (int sl = 0; sl < kSlots; sl++) st[sl] = 0;  // 0 empty, 1 waiting for entry, 2 active
+
+    auto dequeue = [&](int &t, int &qq) -> bool {
+        while (!drained) {
+            int v = 0;
+            if (lane == 0) v = atomicAdd(&a.queues[q * kQueueStride], 1);
+            v = __builtin_amdgcn_readfirstlane(v);
+            if (v < n_tasks) {
+                t = v;
+                qq = q;
+                return true;
+            }
+            if (++empty == kXcds) drained = true;  // this queue is drained: steal from the next
+            else q = (q + 1) & (kXcds - 1);
+        }
+        return false;
+    };
+    // the chain leaves slot sl's segment at absolute position pos: hand it on
+    auto finish = [&](int sl, int pos) {
+        if (lane == 0) {
+            if (tq[sl] + 1 < kXcds)
+                __hip_atomic_store(&w.entry[(long long)tt[sl] * kXcds + tq[sl] + 1], pos + 1,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (nvis[sl]) atomicAdd(&w.row_visited[tt[sl]], nvis[sl]);
+        }
+        st[sl] = 0;
+    };
+    auto start = [&](int sl, int pos) {  // the chain entered the segment at pos
+        const int rel = pos - j0[sl];
+        if (rel >= nseg[sl]) {
+            finish(sl, pos);
+            return;
+        }
+        for (int i = lane; i < 3 * nwords; i += 64) bits0[sl * 3 * nwords + i] = 0ull;
+        r[sl] = rel;
+        st[sl] = 2;
+    };
+
     for (;;) {
-        if (t >= n_tasks) {  // this queue is drained: steal from the next XCD's
-            if (++empty == kXcds) break;
-            q = (q + 1) & (kXcds - 1);
-            t = 0;
-            if (lane == 0) t = atomicAdd(&a.queues[q * kQueueStride], 1);
-            t = __builtin_amdgcn_readfirstlane(t);
+        // 1) refill empty slots, poll the entries of waiting ones
+        int n_active = 0, n_wait = 0;
+#pragma unroll
+        for (int sl = 0; sl < kSlots; sl++) {
+            if (st[sl] == 0) {
+                int t, qq;
+                if (dequeue(t, qq)) {
+                    const int fr = t / w.n_rows, row = t - fr * w.n_rows;
+                    const int2 rd = w.rows[row];
+                    const LevelInfo L = w.levels[rd.x];
+                    const int nxs = (L.nx + kXcds - 1) / kXcds;
+                    tt[sl] = t;
+                    tq[sl] = qq;
+                    frame[sl] = fr;
+                    level[sl] = rd.x;
+                    j0[sl] = min(L.nx, qq * nxs);
+                    nseg[sl] = min(L.nx, j0[sl] + nxs) - j0[sl];
+                    nvis[sl] = 0;
+                    st[sl] = 1;
+                    if (qq == 0) start(sl, 0);
+                }
+            }
+            if (st[sl] == 1) {  // poll once; a lost hand-off must not hang the GPU
+                int e = 0;
+                if (lane == 0)
+                    e = __hip_atomic_load(&w.entry[(long long)tt[sl] * kXcds + tq[sl]], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                e = __builtin_amdgcn_readfirstlane(e);
+                if (e) start(sl, e - 1);
+            }
+            n_active += st[sl] == 2;
+            n_wait += st[sl] == 1;
+        }
+        if (n_active == 0) {
+            if (n_wait == 0) {
+                if (drained) break;
+                continue;
+            }
+            __builtin_amdgcn_s_sleep(4);
+            if (++idle == (1u << 24)) {  // a lost hand-off must not hang the GPU
+#pragma unroll
+                for (int sl = 0; sl < kSlots; sl++)
+                    if (st[sl] == 1) {
+                        if (lane == 0) atomicAdd(w.err, 1);
+                        start(sl, j0[sl]);
+                    }
+                idle = 0;
+            }
             continue;
         }
-        int tn = 0;  // prefetch the next task index
-        if (lane == 0) tn = atomicAdd(&a.queues[q * kQueueStride], 1);
-        const int frame = t / w.n_rows, row = t - frame * w.n_rows;
-        const int2 rd = w.rows[row];
-        const LevelInfo L = w.levels[rd.x];
-        const int y = rd.y, nx = L.nx, nxs = (nx + kXcds - 1) / kXcds;
-        const int j0 = min(nx, q * nxs), j1 = min(nx, j0 + nxs);  // this segment: [j0, j1)
-        const long long gi0 = (long long)frame * w.grid_per_frame + L.grid_base +
-                              (long long)(y / w.step) * nx;
-        // entry: where the chain enters the segment (j0 or j0 + 1), from segment q - 1
-        int pos = SC_ABL_NOWAIT ? j0 : 0;
-        if (q > 0 && !SC_ABL_NOWAIT) {
-            int e = 0;
+        idle = 0;
+
+        // 2) one evaluation round over every active slot's next batch
+#pragma unroll
+        for (int sl = 0; sl < kSlots; sl++) {
             if (lane == 0) {
-                int *ep = &w.entry[(long long)t * kXcds + q];
-                unsigned spins = 0;  // bounded: a lost hand-off must not hang the GPU
-                while ((e = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins == (1u << 26)) {
-                        atomicAdd(w.err, 1);
-                        e = j0 + 1;
-                        break;
-                    }
+                SlotDesc dd{};
+                if (st[sl] == 2) {
+                    const int fr = frame[sl], row = tt[sl] - fr * w.n_rows;
+                    const int2 rd = w.rows[row];
+                    const LevelInfo L = w.levels[level[sl]];
+                    const int jb = j0[sl] + r[sl];  // the batch: jb, jb + 2, ...
+                    dd.t_off = (unsigned)((long long)fr * g.frame4 + rd.y * g.rowp + g.win_cell(jb));
+                    dd.nw = min(kBatch, (nseg[sl] - r[sl] + 1) >> 1);
+                    dd.thr = L.thr;
+                    dd.pre_row = L.pre_row;
+                    dd.pre_col = L.pre_col[jb & 1];
+                    dd.proj = (level[sl] * 2 + (jb & 1)) * a.K;
                 }
+                desc[sl] = dd;
             }
-            pos = __builtin_amdgcn_readfirstlane(e) - 1;
-        }
-        unsigned nvis = 0;
-        if (pos < j1) {
-            const char *Tb = reinterpret_cast<const char *>(a.table + (long long)frame * g.frame4);
-            const unsigned row_off = (unsigned)(y * g.rowp);
-            const int nseg = j1 - j0;
-            for (int i = lane; i < ((nseg + 63) >> 6); i += 64) {
-                evb[i] = 0ull;
-                gdb[i] = 0ull;
-                dtb[i] = 0ull;
-            }
-            wave_sync();
-            const unsigned long long kEven = 0x5555555555555555ull;
-            int r = pos - j0;  // chain position relative to the segment
-            while (r < nseg) {
-                // evaluate the next kBatch windows of r's parity not yet evaluated
-                const int nb = min(kBatch, (nseg - r + 1) >> 1);
-                const WinSet B{row_off + (unsigned)((j0 + r) * cs), nb, 1, 0, 2 * cs,
-                               rd.x, L.thr, L.pre_row, L.pre_col};
-                auto need = [&](int u) {
-                    const int k = r + 2 * u;
-                    return ((evb[k >> 6] >> (k & 63)) & 1ull) == 0ull;
-                };
-                const bool mine = lane < nb && need(lane);
-                eval_windows<LW>(a, B, Tb, Wl, Bl, Ol, P, st_s, surv, st_p, lane, need);
-                wave_sync();
-                if (mine) {  // merge the batch into the segment's bits
-                    const int k = r + 2 * lane, p = st_p[lane];
-                    const float sc = st_s[lane];
-                    bool good = false;
-                    if (p >= 0) {
-                        const double fin = ((double)sc + p + 1) / S;  // ObjDetector.cpp:201
-                        good = !(fin < w.stride_score);               // :214
-                    }
-                    s_seg[k] = sc;
-                    atomicOr(&evb[k >> 6], 1ull << (k & 63));
-                    if (good) atomicOr(&gdb[k >> 6], 1ull << (k & 63));
-                    if (p == S) atomicOr(&dtb[k >> 6], 1ull << (k & 63));  // passed every stage
-                    if (a.st_p) {  // debug: per-window results for the parity dumps
-                        a.st_p[gi0 + j0 + k] = (int8_t)p;
-                        a.st_s[gi0 + j0 + k] = sc;
-                    }
-                }
-                wave_sync();
-                // advance the chain over evaluated windows: from a landing
-                // position it visits every second window until a good one
-                for (;;) {
-                    const int c = r >> 6, b = r & 63;
-                    const unsigned long long par = (b & 1) ? ~kEven : kEven;
-                    const int lim = min(64, nseg - (c << 6));  // bits past the segment
-                    const unsigned long long inseg = lim == 64 ? ~0ull : ((1ull << lim) - 1ull);
-                    const unsigned long long path = par & (~0ull << b) & inseg;
-                    const unsigned long long ev = evb[c];
-                    const unsigned long long unev = path & ~ev, good = path & ev & gdb[c];
-                    const int f = unev ? __builtin_ctzll(unev) : 64;
-                    const int qg = good ? __builtin_ctzll(good) : 64;
-                    unsigned long long vis;
-                    if (f < qg) {  // an unevaluated window: next batch from there
-                        vis = path & ((1ull << f) - 1ull);
-                        r = (c << 6) + f;
-                    } else if (qg < 64) {  // lands on good window qg, continues at qg + 1
-                        vis = path & (qg == 63 ? ~0ull : ((2ull << qg) - 1ull));
-                        const int k = (c << 6) + qg;
-                        if (lane == 0 && ((dtb[c] >> qg) & 1ull)) {  // detection (:203)
-                            const int slot = atomicAdd(&w.counters[0], 1);
-                            atomicAdd(&w.counters[1 + frame], 1);
-                            if (slot < w.capacity) {
-                                sc_det_record rec;
-                                rec.frame = frame;
-                                rec.level = rd.x;
-                                rec.x = (j0 + k) * w.step;
-                                rec.y = y;
-                                rec.w = L.l;
-                                rec.h = L.lh;
-                                rec.stage_reached = S;
-                                rec._pad = 0;
-                                rec.score = ((double)s_seg[k] + S + 1) / S;  // :201
-                                w.out[slot] = rec;
-                            }
-                        }
-                        r = k + 1;
-                    } else {  // every path bit of this word visited
-                        vis = path;
-                        r = lim < 64 ? nseg + (b & 1) : ((c + 1) << 6) + (b & 1);
-                        if (lim < 64) {  // the chain's next landing past the segment
-                            const int last = 63 - __builtin_clzll(path | 1ull);
-                            r = path ? (c << 6) + last + 2 : r;
-                        }
-                    }
-                    nvis += __popcll(vis);
-                    if (w.dbg_v && ((vis >> lane) & 1ull)) w.dbg_v[gi0 + j0 + (c << 6) + lane] = 1;
-                    if (f < qg || r >= nseg) break;
-                }
-            }
-            pos = j0 + r;
-        }
-        // hand the chain to the next segment (one agent-scope word: value + 1)
-        if (lane == 0) {
-            if (q + 1 < kXcds)
-                __hip_atomic_store(&w.entry[(long long)t * kXcds + q + 1], pos + 1, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            if (nvis) atomicAdd(&w.row_visited[t], nvis);
         }
         wave_sync();
-        t = __builtin_amdgcn_readfirstlane(tn);
+        const SlotRows B{desc, kSlots, kBatch, g.ph == g.step ? 2 * cs : cs, a.proj};
+        auto need = [&](int slot) {  // window not evaluated yet (an earlier batch may have)
+            const int sl = slot / kBatch, u = slot - sl * kBatch;
+            int rr = r[0];
+#pragma unroll
+            for (int x = 1; x < kSlots; x++)
+                if (sl == x) rr = r[x];
+            const int k = rr + 2 * u;
+            return ((evb(sl)[k >> 6] >> (k & 63)) & 1ull) == 0ull;
+        };
+        bool mine[kSlots];
+#pragma unroll
+        for (int sl = 0; sl < kSlots; sl++) mine[sl] = st[sl] == 2 && lane < desc[sl].nw && need(sl * kBatch + lane);
+        eval_windows<LW>(a, B, reinterpret_cast<const char *>(a.table), Wl, Bl, Ol, P, st_s, surv,
+                         st_p, lane, need);
+        wave_sync();
+
+        // 3) per slot: merge the batch, advance the chain
+#pragma unroll
+        for (int sl = 0; sl < kSlots; sl++) {
+            if (st[sl] != 2) continue;
+            const int fr = frame[sl], row = tt[sl] - fr * w.n_rows;
+            const int2 rd = w.rows[row];
+            const LevelInfo L = w.levels[level[sl]];
+            const long long gi0 = (long long)fr * w.grid_per_frame + L.grid_base +
+                                  (long long)(rd.y / w.step) * L.nx + j0[sl];
+            unsigned long long *ev_ = evb(sl), *gd_ = gdb(sl), *dt_ = dtb(sl);
+            float *sg = s_seg(sl);
+            if (mine[sl]) {
+                const int k = r[sl] + 2 * lane, p = st_p[sl * kBatch + lane];
+                const float sc = st_s[sl * kBatch + lane];
+                bool good = false;
+                if (p >= 0) {
+                    const double fin = ((double)sc + p + 1) / S;  // ObjDetector.cpp:201
+                    good = !(fin < w.stride_score);               // :214
+                }
+                sg[k] = sc;
+                atomicOr(&ev_[k >> 6], 1ull << (k & 63));
+                if (good) atomicOr(&gd_[k >> 6], 1ull << (k & 63));
+                if (p == S) atomicOr(&dt_[k >> 6], 1ull << (k & 63));  // passed every stage
+                if (a.st_p) {  // debug: per-window results for the parity dumps
+                    a.st_p[gi0 + k] = (int8_t)p;
+                    a.st_s[gi0 + k] = sc;
+                }
+            }
+            wave_sync();
+            int rr = r[sl];
+            const int ns = nseg[sl];
+            for (;;) {  // from a landing position: every second window until a good one
+                const int c = rr >> 6, b = rr & 63;
+                const unsigned long long par = (b & 1) ? ~kEven : kEven;
+                const int lim = min(64, ns - (c << 6));  // bits past the segment
+                const unsigned long long inseg = lim == 64 ? ~0ull : ((1ull << lim) - 1ull);
+                const unsigned long long path = par & (~0ull << b) & inseg;
+                const unsigned long long evw = ev_[c];
+                const unsigned long long unev = path & ~evw, good = path & evw & gd_[c];
+                const int f = unev ? __builtin_ctzll(unev) : 64;
+                const int qg = good ? __builtin_ctzll(good) : 64;
+                unsigned long long vis;
+                if (f < qg) {  // an unevaluated window: next batch from there
+                    vis = path & ((1ull << f) - 1ull);
+                    rr = (c << 6) + f;
+                } else if (qg < 64) {  // lands on good window qg, continues at qg + 1
+                    vis = path & (qg == 63 ? ~0ull : ((2ull << qg) - 1ull));
+                    const int k = (c << 6) + qg;
+                    if (lane == 0 && ((dt_[c] >> qg) & 1ull)) {  // detection (:203)
+                        const int slot = atomicAdd(&w.counters[0], 1);
+                        atomicAdd(&w.counters[1 + w.frame0 + fr], 1);
+                        if (slot < w.capacity) {
+                            sc_det_record rec;
+                            rec.frame = w.frame0 + fr;
+                            rec.level = level[sl];
+                            rec.x = (j0[sl] + k) * w.step;
+                            rec.y = rd.y;
+                            rec.w = L.l;
+                            rec.h = L.lh;
+                            rec.stage_reached = S;
+                            rec._pad = 0;
+                            rec.score = ((double)sg[k] + S + 1) / S;  // :201
+                            w.out[slot] = rec;
+                        }
+                    }
+                    rr = k + 1;
+                } else {  // every path bit of this word visited
+                    vis = path;
+                    if (lim < 64) rr = (c << 6) + (63 - __builtin_clzll(path)) + 2;
+                    else rr = ((c + 1) << 6) + (b & 1);
+                }
+                nvis[sl] += __popcll(vis);
+                if (w.dbg_v && ((vis >> lane) & 1ull)) w.dbg_v[gi0 + (c << 6) + lane] = 1;
+                if (f < qg || rr >= ns) break;
+            }
+            r[sl] = rr;
+            if (rr >= ns) finish(sl, j0[sl] + rr);
+        }
+        wave_sync();
     }
 }
 
