@@ -9,12 +9,13 @@
 //              kStrip pixels; exclusive per-strip prefix ("carry") of the 8
 //              channels (u32, exact) -> carry[frame][y][strip][8].  Also
 //              zeroes table row 0 and column 0.
-//   colstrip : one wave per (frame, strip): for y = 0..H-1 the strip's
-//              gradients again, an exact in-strip prefix (wave scan) plus the
-//              carry gives R_y, then S += R_y in f32 -- the reference's
-//              association order -- and one store per table cell.
-// Lane mapping in both: lane = half*32 + column; half 0 owns channels 0-3
-// (dx, dy), half 1 channels 4-7 (du, dv), i.e. one table half-cell (float4).
+//   colstrip : one wave per (frame, 64-px strip, channel half): for y =
+//              0..H-1 the strip's gradients again, an exact in-strip prefix
+//              (wave scan) plus the carry gives R_y, then S += R_y in f32 --
+//              the reference's association order -- and one store per table
+//              half-cell.
+// rowcarry lanes = half*32 + column, colstrip lanes = column; half 0 owns
+// channels 0-3 (dx, dy), half 1 channels 4-7 (du, dv): one table half-cell.
 //
 // Every f32 operation is the one the reference performs, in its order;
 // compiled with -ffp-contract=off, no fast-math.  Table layout: sc_kernels.hpp.
@@ -119,18 +120,28 @@ __global__ __launch_bounds__(64) void rowcarry_kernel(RowScanArgs a) {
     }
 }
 
+// inclusive prefix sum over the whole wave: the half scan, then row 1's last
+// lane broadcast into rows 2 and 3
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
+    v = half_scan(v);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
+
+// One wave per (frame, 64-column strip, channel half): lane = column, so a
+// row's stores are long runs within each phase plane of the half.
 __global__ __launch_bounds__(64) void colstrip_kernel(RowScanArgs a) {
-    const int s = blockIdx.x, frame = blockIdx.y, lane = threadIdx.x;
-    const int h = lane >> 5, c = lane & 31;
+    const int s = blockIdx.x >> 1, h = blockIdx.x & 1, frame = blockIdx.y, lane = threadIdx.x;
     const TableGeom g = a.g;
-    const int W = g.W, H = g.H, ns = (W + kStrip - 1) / kStrip;
-    const int x = s * kStrip + c;
+    const int W = g.W, H = g.H, ns = (W + kStrip - 1) / kStrip;  // carries per 32-px strip
+    const int x = s * 2 * kStrip + lane;
     const bool live = x < W;
     const int xs = live ? x : W - 1;  // dead lanes still join the scan with zeros
     const uint8_t *img = a.frames + (long long)frame * a.frame_bytes;
     float4 *cellp = a.table + (long long)frame * g.frame4 + g.at(x + 1, h);  // row 0 of the column
+    // the exclusive carry at column 64*s is the 32-px strip 2*s's
     const uint4 *cin = reinterpret_cast<const uint4 *>(a.carry) + (long long)frame * H * ns * 2 +
-                       (long long)s * 2 + h;
+                       (long long)(2 * s) * 2 + h;
     // software pipeline: the loads of block b+1 are in flight while block b
     // is scanned and stored
     Px4 pa[kColUnroll];
@@ -153,8 +164,8 @@ __global__ __launch_bounds__(64) void colstrip_kernel(RowScanArgs a) {
         for (int k = 0; k < kColUnroll; k++) {
             const int y = y0 + k;  // rows past H: harmless extra steps, not stored
             uint2 p = live ? grad_packed(pa[k]) : make_uint2(0u, 0u);
-            p.x = half_scan(p.x);
-            p.y = half_scan(p.y);
+            p.x = wave_scan(p.x);  // 16-bit channel pairs: 64 px x 255 < 2^16
+            p.y = wave_scan(p.y);
             // R_y[x+1] exact (< 2^24), then the f32 column step
             S0 = S0 + (float)(ca[k].x + (p.x & 0xffffu));
             S1 = S1 + (float)(ca[k].y + (p.x >> 16));
@@ -177,8 +188,8 @@ void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
 }
 
 void launch_colscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
-    const int ns = (a.g.W + kStrip - 1) / kStrip;
-    hipLaunchKernelGGL(colstrip_kernel, dim3(ns, n_frames), dim3(64), 0, s, a);
+    const int ns64 = (a.g.W + 2 * kStrip - 1) / (2 * kStrip);
+    hipLaunchKernelGGL(colstrip_kernel, dim3(ns64 * 2, n_frames), dim3(64), 0, s, a);
 }
 
 }  // namespace sc
