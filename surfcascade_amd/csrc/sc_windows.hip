@@ -455,7 +455,10 @@ __global__ __launch_bounds__(64) void walk_kernel(WalkArgs a) {
 #define SC_CHAIN_SLOTS 2
 #endif
 constexpr int kSlots = SC_CHAIN_SLOTS;
-constexpr int kBatch = 64;  // chain kernel: windows of one parity per slot and round
+#ifndef SC_CHAIN_BATCH
+#define SC_CHAIN_BATCH 64
+#endif
+constexpr int kBatch = SC_CHAIN_BATCH;  // chain kernel: windows of one parity per slot and round
 
 // chain kernel LDS per wave: P f32[kItemBuf] | st_s f32[kSlots*kBatch] |
 // surv u32[kSlots*kBatch] | per slot: segment scores f32[SEGA], evaluated /
@@ -627,7 +630,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
                     dd.nw = min(kBatch, (nseg[sl] - r[sl] + 1) >> 1);
                     dd.thr = L.thr;
                     dd.pre_row = L.pre_row;
-                    dd.pre_col = L.pre_col[jb & 1];
+                    dd.pre_col = (jb & 1) ? L.pre_col[1] : L.pre_col[0];  // (no dynamic index: scratch)
                     dd.proj = (level[sl] * 2 + (jb & 1)) * a.K;
                 }
                 desc[sl] = dd;
