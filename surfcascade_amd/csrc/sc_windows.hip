@@ -121,7 +121,8 @@ struct SlotDesc {
     float thr;
     int pre_row, pre_col;
     int proj;        // (level * 2 + parity) * K
-    int pad[2];
+    int r;           // the batch's first window, relative to the segment
+    int pad;
 };
 struct SlotRows {
     const SlotDesc *d;
@@ -466,7 +467,8 @@ constexpr int kBatch = SC_CHAIN_BATCH;  // chain kernel: windows of one parity p
 __host__ __device__ inline size_t chain_wave_bytes(int seg_max) {
     const size_t sa = (size_t)((seg_max + 63) & ~63);
     return (size_t)kItemBuf * 4 + (size_t)kSlots * kBatch * 9 +
-           (size_t)kSlots * (sa * 4 + sa / 64 * 24) + kSlots * sizeof(SlotDesc) + 64;
+           (size_t)kSlots * (sa * 4 + sa / 64 * 24) + kSlots * sizeof(SlotDesc) +
+           (size_t)kSlots * 9 * 4 + 64;
 }
 
 // Lazy grid (the default detect path).  The reference evaluates only the
@@ -506,7 +508,8 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
     float *s_seg0 = reinterpret_cast<float *>(surv + kSlots * kBatch);
     unsigned long long *bits0 = reinterpret_cast<unsigned long long *>(s_seg0 + kSlots * sa);
     SlotDesc *desc = reinterpret_cast<SlotDesc *>(bits0 + kSlots * 3 * nwords);
-    int8_t *st_p = reinterpret_cast<int8_t *>(desc + kSlots);
+    int *park = reinterpret_cast<int *>(desc + kSlots);  // slot state parked across a round
+    int8_t *st_p = reinterpret_cast<int8_t *>(park + kSlots * 9);
     auto s_seg = [&](int sl) { return s_seg0 + sl * sa; };
     auto evb = [&](int sl) { return bits0 + (sl * 3 + 0) * nwords; };
     auto gdb = [&](int sl) { return bits0 + (sl * 3 + 1) * nwords; };
@@ -632,6 +635,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
                     dd.pre_row = L.pre_row;
                     dd.pre_col = (jb & 1) ? L.pre_col[1] : L.pre_col[0];  // (no dynamic index: scratch)
                     dd.proj = (level[sl] * 2 + (jb & 1)) * a.K;
+                    dd.r = r[sl];
                 }
                 desc[sl] = dd;
             }
@@ -640,19 +644,39 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
         const SlotRows B{desc, kSlots, kBatch, g.ph == g.step ? 2 * cs : cs, a.proj};
         auto need = [&](int slot) {  // window not evaluated yet (an earlier batch may have)
             const int sl = slot / kBatch, u = slot - sl * kBatch;
-            int rr = r[0];
-#pragma unroll
-            for (int x = 1; x < kSlots; x++)
-                if (sl == x) rr = r[x];
-            const int k = rr + 2 * u;
+            const int k = desc[sl].r + 2 * u;
             return ((evb(sl)[k >> 6] >> (k & 63)) & 1ull) == 0ull;
         };
         bool mine[kSlots];
 #pragma unroll
         for (int sl = 0; sl < kSlots; sl++) mine[sl] = st[sl] == 2 && lane < desc[sl].nw && need(sl * kBatch + lane);
+        // park the slot state in LDS across the evaluation: it would otherwise
+        // stay live in SGPRs / VGPR lanes through the register-heavy item loop
+        if (lane == 0) {
+#pragma unroll
+            for (int sl = 0; sl < kSlots; sl++) {
+                int *pk = park + sl * 9;
+                pk[0] = st[sl]; pk[1] = tq[sl]; pk[2] = tt[sl]; pk[3] = r[sl]; pk[4] = j0[sl];
+                pk[5] = nseg[sl]; pk[6] = frame[sl]; pk[7] = level[sl]; pk[8] = (int)nvis[sl];
+            }
+        }
+        wave_sync();
         eval_windows<LW>(a, B, reinterpret_cast<const char *>(a.table), Wl, Bl, Ol, P, st_s, surv,
                          st_p, lane, need);
         wave_sync();
+#pragma unroll
+        for (int sl = 0; sl < kSlots; sl++) {
+            const int *pk = park + sl * 9;
+            st[sl] = __builtin_amdgcn_readfirstlane(pk[0]);
+            tq[sl] = __builtin_amdgcn_readfirstlane(pk[1]);
+            tt[sl] = __builtin_amdgcn_readfirstlane(pk[2]);
+            r[sl] = __builtin_amdgcn_readfirstlane(pk[3]);
+            j0[sl] = __builtin_amdgcn_readfirstlane(pk[4]);
+            nseg[sl] = __builtin_amdgcn_readfirstlane(pk[5]);
+            frame[sl] = __builtin_amdgcn_readfirstlane(pk[6]);
+            level[sl] = __builtin_amdgcn_readfirstlane(pk[7]);
+            nvis[sl] = (unsigned)__builtin_amdgcn_readfirstlane(pk[8]);
+        }
 
         // 3) per slot: merge the batch, advance the chain
 #pragma unroll
