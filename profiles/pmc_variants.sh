@@ -14,7 +14,7 @@ for spec in "${V[@]}"; do
   for grp in "TCC_EA0_RDREQ TCC_HIT TCC_MISS" "SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES" \
              "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum"; do
     tag=$(echo $grp | cut -c1-6)
-    export $envs
+    [ -n "$envs" ] && export $envs
     SURFCASCADE_LIB="$R/surfcascade_amd/lib/variants/$var/libsurfcascade.so" timeout -k 10 200 \
       rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$R/$OUT/$name.$tag" -o pmc \
       -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu "$@" > /dev/null 2>&1 || exit 1

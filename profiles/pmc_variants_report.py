@@ -11,7 +11,7 @@ for f in glob.glob(os.path.join(d, "*", "pmc_counter_collection.csv")):
     v = os.path.basename(os.path.dirname(f)).split(".")[0]
     acc = collections.defaultdict(list)
     for row in csv.DictReader(open(f)):
-        if "cascade_kernel" in row["Kernel_Name"] or "window_kernel" in row["Kernel_Name"]:
+        if any(k in row["Kernel_Name"] for k in ("cascade_kernel", "window_kernel", "chain_kernel")):
             acc[row["Counter_Name"]].append(float(row["Counter_Value"]))
     for k, x in acc.items():
         res[v][k] = sum(x) / len(x) / frames

@@ -202,8 +202,10 @@ void build_geometry(sc_detector *d, int W, int H) {
         t.step = ng.step;
         // parity-split phase planes: the lazy grid's batches (one parity,
         // windows 2 apart) then read consecutive cells
-        const char *ep = std::getenv("SC_PHASES");  // tuning override: 1 = step planes
-        t.ph = (ep && std::atoi(ep) == 1) ? ng.step : 2 * ng.step;
+        // (the full grid -- dumps, the miner -- reads consecutive windows: step planes)
+        const char *ep = std::getenv("SC_PHASES");  // tuning override: 1 or 2 planes per step
+        const int mult = ep ? (std::atoi(ep) == 1 ? 1 : 2) : (d->lazy ? 2 : 1);
+        t.ph = mult * ng.step;
         const int Q = (W + 1 + t.ph - 1) / t.ph;
         t.Qp = (Q + 15) & ~15;
         t.rowp = 2 * t.ph * t.Qp;
