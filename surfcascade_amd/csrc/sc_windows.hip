@@ -460,15 +460,17 @@ constexpr int kSlots = SC_CHAIN_SLOTS;
 #define SC_CHAIN_BATCH 64
 #endif
 constexpr int kBatch = SC_CHAIN_BATCH;  // chain kernel: windows of one parity per slot and round
+static_assert(kBatch % 4 == 0 && kItemBuf % 4 == 0, "chain LDS carve: keep the u64 bit arrays aligned");
 
 // chain kernel LDS per wave: P f32[kItemBuf] | st_s f32[kSlots*kBatch] |
 // surv u32[kSlots*kBatch] | per slot: segment scores f32[SEGA], evaluated /
 // good / detection bits u64[SEGA/64] x 3 | SlotDesc[kSlots] | st_p i8[kSlots*kBatch]
 __host__ __device__ inline size_t chain_wave_bytes(int seg_max) {
     const size_t sa = (size_t)((seg_max + 63) & ~63);
-    return (size_t)kItemBuf * 4 + (size_t)kSlots * kBatch * 9 +
-           (size_t)kSlots * (sa * 4 + sa / 64 * 24) + kSlots * sizeof(SlotDesc) +
-           (size_t)kSlots * 9 * 4 + 64;
+    const size_t b = (size_t)kItemBuf * 4 + (size_t)kSlots * kBatch * 9 +
+                     (size_t)kSlots * (sa * 4 + sa / 64 * 24) + kSlots * sizeof(SlotDesc) +
+                     (size_t)kSlots * 9 * 4 + 64;
+    return (b + 15) & ~(size_t)15;  // every wave's block 16-B aligned (64-bit LDS atomics)
 }
 
 // Lazy grid (the default detect path).  The reference evaluates only the
