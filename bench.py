@@ -218,7 +218,9 @@ def main():
                        "levels": args.levels, "parallelism": "frame-sharded dp%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "cascade_kernel", "avg_launch_ms": avg_win_s * 1e3,
+                         "kernel": ("cascade_kernel" if os.environ.get("SC_FULL_GRID", "0") != "0"
+                                    else "chain_kernel"),
+                         "avg_launch_ms": avg_win_s * 1e3,
                          "bytes_per_launch": tab_bytes * B,
                          "pipeline_achieved": pipe_bytes * B / pipe_s / 1e9,
                          "pipeline_frac": pipe_bytes * B / pipe_s / 1e9 / HBM_PEAK_GBS},

@@ -13,7 +13,8 @@ import glob
 import json
 import os
 
-KERNELS = {"window_kernel": "windows", "cascade_kernel": "windows", "walk_kernel": "walk",
+KERNELS = {"window_kernel": "windows", "cascade_kernel": "windows", "chain_kernel": "windows",
+           "walk_kernel": "walk",
            "rowscan_kernel": "rowscan", "colscan_kernel": "colscan",
            "rowcarry_kernel": "rowscan", "colstrip_kernel": "colscan"}
 
