@@ -557,7 +557,9 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     if (lazy) {  // the walk drives the cascade: one chain kernel per chunk of frames
         const size_t n_rows = g.rows.size();
         // table offsets are 32-bit byte offsets from the chunk's first frame
-        const int chunk = (int)std::max<long long>(1, (1ll << 28) / g.tg.frame4);
+        int chunk = (int)std::max<long long>(1, (1ll << 28) / g.tg.frame4);
+        if (const char *e = std::getenv("SC_CHAIN_CHUNK"))  // testing: smaller frame chunks
+            chunk = std::max(1, std::min(chunk, std::atoi(e)));
         d->d_entry.ensure(n_rows * std::min(chunk, n) * sc::kXcds + 1);
         if (d->debug) {  // dumps: unevaluated windows read -2, unvisited 0
             HIPCHK(hipMemsetAsync(d->d_st_p.p, 0xFE, (size_t)g.grid * n, d->stream));

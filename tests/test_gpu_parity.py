@@ -141,6 +141,27 @@ def test_permissive_cascade_many_detections(sc, oracle, face_cascade, monkeypatc
     assert det.info("visited") == nvis
 
 
+def test_lazy_grid_wide_rows_and_frame_chunks(sc, oracle, face_cascade, monkeypatch):
+    """Row segments wider than one 64-window batch per parity (several rounds per
+    task) and a batch split into several chain-kernel launches (frame chunks)."""
+    monkeypatch.setenv("SC_CHAIN_CHUNK", "2")
+    from surfcascade_amd import synth
+    c = face_cascade
+    theta = np.full(c.n_stages, 0.3, np.float32)  # many good windows: frequent parity switches
+    text = synth.write_cfg(synth.cascade_tree(c.n_weak, theta, c.patch_index, c.w, c.bias))
+    casc_or = oracle.cascade_from_cfg(text)
+    frames = np.stack([_frame(3000, 160, 700 + k) for k in range(5)])
+    det = sc.Detector(sc.Model.parse(text), sc.ScanParams(n_levels=3))
+    batch = det.detect_batch(frames)
+    vis = 0
+    for k in range(5):
+        ref, nv = oracle.detect(oracle.integral(frames[k]), casc_or, oracle.Params(n_levels=3))
+        assert _det_set(batch[k]) == _det_set(ref)
+        vis += nv
+    assert det.info("visited") == vis
+    assert sum(len(b) for b in batch) > 100
+
+
 def test_batch_equals_single(sc, oracle, face_cascade):
     frames = np.stack([_frame(640, 480, 100 + k) for k in range(4)])
     det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=5))
