@@ -120,6 +120,7 @@ struct sc_detector {
     DevBuf<unsigned> d_visited;  // per (frame, row): windows the x chain visited
     DevBuf<int> d_queues;       // per-XCD task counters of the cascade kernel
     DevBuf<int> d_entry;        // chain kernel: per (row, segment) chain entry + 1
+    DevBuf<unsigned long long> d_prof;  // chain kernel phase cycles (SC_PROF_CHAIN builds)
     long long err_word = -1;    // chain kernel: index of the hand-off watchdog word in d_entry
     DevBuf<int8_t> d_st_p;      // per grid window: stage reached (-1 prefilter reject)
     DevBuf<float> d_st_s;       // per grid window: last stage score
@@ -152,7 +153,7 @@ struct sc_detector {
         d_feat.release();
         d_frames.release(); d_table.release(); d_carry.release(); d_out.release(); d_counters.release();
         d_visited.release(); d_queues.release(); d_entry.release(); d_st_p.release(); d_st_s.release();
-        d_dbg_v.release();
+        d_dbg_v.release(); d_prof.release();
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -331,6 +332,18 @@ void build_geometry(sc_detector *d, int W, int H) {
         }
         ng.n_bands = (int)(ng.tasks.size() / nseg);
     }
+    if (const char *e = std::getenv("SC_ROW_ORDER")) {  // experiment: chain/walk row order
+        // 1: y-major over levels; 2: blocks of SC_ROW_BLOCK grid rows, level-major inside
+        const int mode = std::atoi(e);
+        const char *eb = std::getenv("SC_ROW_BLOCK");
+        const int blk = std::max(1, eb ? std::atoi(eb) : 16) * ng.step;
+        if (mode == 1)
+            std::stable_sort(ng.rows.begin(), ng.rows.end(),
+                             [](const int2 &a, const int2 &b) { return a.y < b.y; });
+        else if (mode == 2)
+            std::stable_sort(ng.rows.begin(), ng.rows.end(),
+                             [blk](const int2 &a, const int2 &b) { return a.y / blk < b.y / blk; });
+    }
     d->d_tasks.ensure(std::max<size_t>(ng.tasks.size(), 1));
     if (!ng.tasks.empty())
         HIPCHK(hipMemcpyAsync(d->d_tasks.p, ng.tasks.data(), ng.tasks.size() * sizeof(sc::TaskDesc),
@@ -464,7 +477,7 @@ void ensure_buffers(sc_detector *d, int n) {
     d->d_carry.ensure((size_t)n * g.H * ((g.W + sc::kStrip - 1) / sc::kStrip) * 8);
     d->d_counters.ensure((size_t)n + 1);
     d->d_visited.ensure(std::max<size_t>(g.rows.size() * n, 1));
-    d->d_queues.ensure(sc::kXcds * sc::kQueueStride);
+    d->d_queues.ensure(sc::kQueueWords);
     d->d_st_p.ensure(std::max<size_t>((size_t)g.grid * n, 1));
     d->d_st_s.ensure(std::max<size_t>((size_t)g.grid * n, 1));
     if (d->debug) d->d_dbg_v.ensure(std::max<size_t>((size_t)g.grid * n, 1));
@@ -527,9 +540,9 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     ca.queues = d->d_queues.p;
     ca.st_p = d->d_st_p.p;
     ca.st_s = d->d_st_s.p;
-    HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kXcds * sc::kQueueStride, d->stream));
+    HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kQueueWords, d->stream));
     const int seg_max = (g.nx_max + sc::kXcds - 1) / sc::kXcds;  // chain kernel segments
-    const bool lazy = d->lazy && sc::chain_lds_bytes(d->K, seg_max) <= 160 * 1024;
+    const bool lazy = d->lazy && sc::chain_lds_bytes(d->K, seg_max, g.n_levels) <= 160 * 1024;
     if (!lazy) {
         timed_begin(d, &e0);
         sc::launch_cascade(ca, d->device, d->stream);
@@ -542,6 +555,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     wk.rows = d->d_rows.p;
     wk.levels = d->d_levels.p;
     wk.n_rows = (int)g.rows.size();
+    wk.n_levels = g.n_levels;
     wk.n_stages = d->S;
     wk.step = g.step;
     wk.stride_score = d->prm.stride_score;
@@ -582,9 +596,16 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             d->err_word = (long long)(n_rows * std::min(chunk, n) * sc::kXcds);
             wc.err = d->d_entry.p + d->err_word;
             wc.frame0 = f0;
+            if (std::getenv("SC_PROF_CHAIN")) {  // profiling builds: cumulative phase cycles
+                if (!d->d_prof.p) {
+                    d->d_prof.ensure(8);
+                    HIPCHK(hipMemsetAsync(d->d_prof.p, 0, 8 * sizeof(unsigned long long), d->stream));
+                }
+                wc.prof = d->d_prof.p;
+            }
             HIPCHK(hipMemsetAsync(d->d_entry.p, 0, sizeof(int) * (n_rows * nc * sc::kXcds + 1) , d->stream));
             if (f0 > 0)
-                HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kXcds * sc::kQueueStride,
+                HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kQueueWords,
                                       d->stream));
             sc::launch_chain(cc, wc, d->device, d->stream);
             HIPCHK(hipGetLastError());
@@ -604,6 +625,12 @@ void check_chain(sc_detector *d) {
     int err = 0;
     HIPCHK(hipMemcpy(&err, d->d_entry.p + d->err_word, sizeof(int), hipMemcpyDeviceToHost));
     if (err) throw Error{SC_ERR_DEVICE, "chain kernel: " + std::to_string(err) + " segment hand-off(s) timed out"};
+    if (d->d_prof.p) {
+        unsigned long long pc[8];
+        HIPCHK(hipMemcpy(pc, d->d_prof.p, sizeof(pc), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "SC_PROF_CHAIN idle %llu setup %llu eval %llu merge %llu rounds %llu slots %llu "
+                     "deq %llu poll %llu\n", pc[0], pc[1], pc[2], pc[3], pc[4], pc[5], pc[6], pc[7]);
+    }
 }
 
 bool rec_less(const sc_det_record &a, const sc_det_record &b) {

@@ -25,6 +25,8 @@ namespace sc {
 
 constexpr int kXcds = 8;          // MI355X: 8 XCDs, one L2 each
 constexpr int kQueueStride = 64;  // ints between per-XCD queue words (own 256-B line each)
+constexpr int kMaxSubQ = 8;       // chain kernel: dequeue counters per XCD queue, at most
+constexpr int kQueueWords = kXcds * kMaxSubQ * kQueueStride;  // the queue buffer
 
 struct TableGeom {
     int W, H, step;
@@ -124,6 +126,7 @@ struct WalkArgs {
     const int2 *rows;
     const LevelInfo *levels;
     int n_rows, n_stages, step;
+    int n_levels;
     double stride_score;
     long long grid_per_frame;
     const int8_t *st_p;
@@ -137,6 +140,7 @@ struct WalkArgs {
     int *entry;      // chain kernel: [frame*rows][kXcds] chain entry + 1 per segment (zeroed)
     int *err;        // chain kernel: hand-off timeouts (must stay 0)
     int frame0;      // chain kernel: first frame of this launch (record frame index)
+    unsigned long long *prof;  // chain kernel, SC_PROF_CHAIN builds: phase cycle totals (or null)
 };
 
 // Hard-negative mining (sc_mine.hip, FillNegSamples): candidate selection
@@ -183,7 +187,7 @@ void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s);
 // cascade args' st_p / st_s, when not null, receive the evaluated windows
 // (others keep the caller's fill).  Returns the number of workgroups.
 int launch_chain(const CascadeArgs &a, const WalkArgs &w, int device, hipStream_t s);
-size_t chain_lds_bytes(int K, int seg_max);
+size_t chain_lds_bytes(int K, int seg_max, int n_levels);
 size_t cascade_lds_bytes(int K, int strip_max, int band_rows);
 
 }  // namespace sc

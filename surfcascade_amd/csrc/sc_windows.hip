@@ -452,6 +452,31 @@ __global__ __launch_bounds__(64) void walk_kernel(WalkArgs a) {
     if (lane == 0) a.row_visited[blockIdx.x] = (unsigned)nvis;
 }
 
+#ifndef SC_PROF_CHAIN  // profiling builds: per-phase s_memtime totals into WalkArgs::prof
+#define SC_PROF_CHAIN 0
+#endif
+#if SC_PROF_CHAIN
+#define SC_PROF(acc)                                               \
+    do {                                                           \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        acc += t_ - t_last;                                        \
+        t_last = t_;                                               \
+    } while (0)
+#else
+#define SC_PROF(acc) \
+    do {             \
+    } while (0)
+#endif
+
+#ifndef SC_ABL_EXTRA_RT
+#define SC_ABL_EXTRA_RT 0
+#endif
+#ifndef SC_SUBQ  // chain kernel: dequeue counters per XCD queue
+#define SC_SUBQ 1
+#endif
+constexpr int kSubQ = SC_SUBQ;
+static_assert(kSubQ >= 1 && kSubQ <= kMaxSubQ, "sub-queue count");
+
 #ifndef SC_CHAIN_SLOTS  // chain kernel: rows (tasks) a wave advances together
 #define SC_CHAIN_SLOTS 2
 #endif
@@ -469,7 +494,7 @@ __host__ __device__ inline size_t chain_wave_bytes(int seg_max) {
     const size_t sa = (size_t)((seg_max + 63) & ~63);
     const size_t b = (size_t)kItemBuf * 4 + (size_t)kSlots * kBatch * 9 +
                      (size_t)kSlots * (sa * 4 + sa / 64 * 24) + kSlots * sizeof(SlotDesc) +
-                     (size_t)kSlots * 9 * 4 + 64;
+                     (size_t)kSlots * 10 * 4 + 64;
     return (b + 15) & ~(size_t)15;  // every wave's block 16-B aligned (64-bit LDS atomics)
 }
 
@@ -500,7 +525,11 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
     float4 *Wl;
     double *Bl;
     int16_t *Ol;
-    stage_model<LW>(a, smem, Wl, Bl, Ol);
+    // the level table in LDS: slot descriptors and merges read it every round
+    LevelInfo *Lv = reinterpret_cast<LevelInfo *>(smem + model_lds_bytes(a.K, LW) +
+                                                  kWavesPerWg * chain_wave_bytes(w.row_max));
+    for (int i = threadIdx.x; i < w.n_levels; i += kCascadeThreads) Lv[i] = w.levels[i];
+    stage_model<LW>(a, smem, Wl, Bl, Ol);  // (its barrier covers Lv)
 
     const int sa = (w.row_max + 63) & ~63, nwords = sa >> 6;  // row_max: widest segment
     unsigned char *ws = smem + model_lds_bytes(a.K, LW) + (size_t)wv * chain_wave_bytes(w.row_max);
@@ -511,7 +540,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
     unsigned long long *bits0 = reinterpret_cast<unsigned long long *>(s_seg0 + kSlots * sa);
     SlotDesc *desc = reinterpret_cast<SlotDesc *>(bits0 + kSlots * 3 * nwords);
     int *park = reinterpret_cast<int *>(desc + kSlots);  // slot state parked across a round
-    int8_t *st_p = reinterpret_cast<int8_t *>(park + kSlots * 9);
+    int8_t *st_p = reinterpret_cast<int8_t *>(park + kSlots * 10);
     auto s_seg = [&](int sl) { return s_seg0 + sl * sa; };
     auto evb = [&](int sl) { return bits0 + (sl * 3 + 0) * nwords; };
     auto gdb = [&](int sl) { return bits0 + (sl * 3 + 1) * nwords; };
@@ -521,29 +550,45 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
     const int S = a.n_stages, cs = g.cs;
     const int n_tasks = w.n_rows * a.n_frames;  // per segment queue, in row order
     const unsigned long long kEven = 0x5555555555555555ull;
+    // queue of XCD q: segment q of every row, in row order, dealt through
+    // kSubQ counters on separate lines (sub-queue u: tasks u, u + kSubQ, ...;
+    // a few hundred waves per XCD dequeuing through one atomic word
+    // serialise on its line).  A drained sub-queue sends the wave on to the
+    // next one, then to the other XCDs' queues.
     int q = (int)xcc_id(), empty = 0;
+    int u = (int)((blockIdx.x / kXcds * kWavesPerWg + wv) % kSubQ);
     bool drained = false;
     unsigned idle = 0;  // rounds with every task waiting for its entry
+#if SC_PROF_CHAIN
+    unsigned long long c_idle = 0, c_setup = 0, c_eval = 0, c_merge = 0, n_rounds = 0, n_slots = 0;
+    unsigned long long c_deq = 0, c_poll = 0;
+    unsigned long long t_last = __builtin_amdgcn_s_memtime();
+#endif
 
     // per-slot task state (wave-uniform)
     int st[kSlots], tq[kSlots], tt[kSlots], r[kSlots], j0[kSlots], nseg[kSlots];
-    int frame[kSlots], level[kSlots];
+    int frame[kSlots], level[kSlots], ys[kSlots];
     unsigned nvis[kSlots];
 #pragma unroll
     for (int sl = 0; sl < kSlots; sl++) st[sl] = 0;  // 0 empty, 1 waiting for entry, 2 active
 
-    auto dequeue = [&](int &t, int &qq) -> bool {
+    auto dequeue = [&](int &t, int &qq, int2 &rd) -> bool {
         while (!drained) {
             int v = 0;
-            if (lane == 0) v = atomicAdd(&a.queues[q * kQueueStride], 1);
-            v = __builtin_amdgcn_readfirstlane(v);
+            if (lane == 0) v = atomicAdd(&a.queues[(q * kSubQ + u) * kQueueStride], 1);
+            v = __builtin_amdgcn_readfirstlane(v) * kSubQ + u;
             if (v < n_tasks) {
                 t = v;
                 qq = q;
+                rd = w.rows[v % w.n_rows];
                 return true;
             }
-            if (++empty == kXcds) drained = true;  // this queue is drained: steal from the next
-            else q = (q + 1) & (kXcds - 1);
+            if (++empty == kXcds * kSubQ) {  // every sub-queue drained
+                drained = true;
+            } else if (++u == kSubQ) {
+                u = 0;
+                q = (q + 1) & (kXcds - 1);
+            }
         }
         return false;
     };
@@ -575,21 +620,21 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
         for (int sl = 0; sl < kSlots; sl++) {
             if (st[sl] == 0) {
                 int t, qq;
-                if (dequeue(t, qq)) {
-                    const int fr = t / w.n_rows, row = t - fr * w.n_rows;
-                    const int2 rd = w.rows[row];
-                    const LevelInfo L = w.levels[rd.x];
-                    const int nxs = (L.nx + kXcds - 1) / kXcds;
+                int2 rd;
+                if (dequeue(t, qq, rd)) {
+                    const int nx = Lv[rd.x].nx, nxs = (nx + kXcds - 1) / kXcds;
                     tt[sl] = t;
                     tq[sl] = qq;
-                    frame[sl] = fr;
+                    frame[sl] = t / w.n_rows;
                     level[sl] = rd.x;
-                    j0[sl] = min(L.nx, qq * nxs);
-                    nseg[sl] = min(L.nx, j0[sl] + nxs) - j0[sl];
+                    ys[sl] = rd.y;
+                    j0[sl] = min(nx, qq * nxs);
+                    nseg[sl] = min(nx, j0[sl] + nxs) - j0[sl];
                     nvis[sl] = 0;
                     st[sl] = 1;
                     if (qq == 0) start(sl, 0);
                 }
+                SC_PROF(c_deq);
             }
             if (st[sl] == 1) {  // poll once; a lost hand-off must not hang the GPU
                 int e = 0;
@@ -598,11 +643,13 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
                                           __HIP_MEMORY_SCOPE_AGENT);
                 e = __builtin_amdgcn_readfirstlane(e);
                 if (e) start(sl, e - 1);
+                SC_PROF(c_poll);
             }
             n_active += st[sl] == 2;
             n_wait += st[sl] == 1;
         }
         if (n_active == 0) {
+            SC_PROF(c_idle);
             if (n_wait == 0) {
                 if (drained) break;
                 continue;
@@ -622,16 +669,23 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
         idle = 0;
 
         // 2) one evaluation round over every active slot's next batch
+#if SC_ABL_EXTRA_RT  // timing ablation: SC_ABL_EXTRA_RT dependent round trips to L2 per round
+#pragma unroll
+        for (int i = 0; i < SC_ABL_EXTRA_RT; i++) {
+            int v = 0;  // (word 1 of this XCD's queue line: unused, stays 0)
+            if (lane == 0) v = atomicAdd(&a.queues[(q * kSubQ + u) * kQueueStride + 1], 0);
+            v = __builtin_amdgcn_readfirstlane(v);
+            if (v == 0x7fffffff) drained = true;
+        }
+#endif
 #pragma unroll
         for (int sl = 0; sl < kSlots; sl++) {
             if (lane == 0) {
                 SlotDesc dd{};
                 if (st[sl] == 2) {
-                    const int fr = frame[sl], row = tt[sl] - fr * w.n_rows;
-                    const int2 rd = w.rows[row];
-                    const LevelInfo L = w.levels[level[sl]];
+                    const LevelInfo &L = Lv[level[sl]];
                     const int jb = j0[sl] + r[sl];  // the batch: jb, jb + 2, ...
-                    dd.t_off = (unsigned)((long long)fr * g.frame4 + rd.y * g.rowp + g.win_cell(jb));
+                    dd.t_off = (unsigned)((long long)frame[sl] * g.frame4 + ys[sl] * g.rowp + g.win_cell(jb));
                     dd.nw = min(kBatch, (nseg[sl] - r[sl] + 1) >> 1);
                     dd.thr = L.thr;
                     dd.pre_row = L.pre_row;
@@ -657,18 +711,25 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
         if (lane == 0) {
 #pragma unroll
             for (int sl = 0; sl < kSlots; sl++) {
-                int *pk = park + sl * 9;
+                int *pk = park + sl * 10;
                 pk[0] = st[sl]; pk[1] = tq[sl]; pk[2] = tt[sl]; pk[3] = r[sl]; pk[4] = j0[sl];
                 pk[5] = nseg[sl]; pk[6] = frame[sl]; pk[7] = level[sl]; pk[8] = (int)nvis[sl];
+                pk[9] = ys[sl];
             }
         }
         wave_sync();
+        SC_PROF(c_setup);
         eval_windows<LW>(a, B, reinterpret_cast<const char *>(a.table), Wl, Bl, Ol, P, st_s, surv,
                          st_p, lane, need);
         wave_sync();
+        SC_PROF(c_eval);
+#if SC_PROF_CHAIN
+        n_rounds++;
+        n_slots += n_active;
+#endif
 #pragma unroll
         for (int sl = 0; sl < kSlots; sl++) {
-            const int *pk = park + sl * 9;
+            const int *pk = park + sl * 10;
             st[sl] = __builtin_amdgcn_readfirstlane(pk[0]);
             tq[sl] = __builtin_amdgcn_readfirstlane(pk[1]);
             tt[sl] = __builtin_amdgcn_readfirstlane(pk[2]);
@@ -678,17 +739,17 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
             frame[sl] = __builtin_amdgcn_readfirstlane(pk[6]);
             level[sl] = __builtin_amdgcn_readfirstlane(pk[7]);
             nvis[sl] = (unsigned)__builtin_amdgcn_readfirstlane(pk[8]);
+            ys[sl] = __builtin_amdgcn_readfirstlane(pk[9]);
         }
 
         // 3) per slot: merge the batch, advance the chain
 #pragma unroll
         for (int sl = 0; sl < kSlots; sl++) {
             if (st[sl] != 2) continue;
-            const int fr = frame[sl], row = tt[sl] - fr * w.n_rows;
-            const int2 rd = w.rows[row];
-            const LevelInfo L = w.levels[level[sl]];
+            const int fr = frame[sl], y = ys[sl];
+            const LevelInfo &L = Lv[level[sl]];
             const long long gi0 = (long long)fr * w.grid_per_frame + L.grid_base +
-                                  (long long)(rd.y / w.step) * L.nx + j0[sl];
+                                  (long long)(y / w.step) * L.nx + j0[sl];
             unsigned long long *ev_ = evb(sl), *gd_ = gdb(sl), *dt_ = dtb(sl);
             float *sg = s_seg(sl);
             if (mine[sl]) {
@@ -736,7 +797,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
                             rec.frame = w.frame0 + fr;
                             rec.level = level[sl];
                             rec.x = (j0[sl] + k) * w.step;
-                            rec.y = rd.y;
+                            rec.y = y;
                             rec.w = L.l;
                             rec.h = L.lh;
                             rec.stage_reached = S;
@@ -759,7 +820,20 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
             if (rr >= ns) finish(sl, j0[sl] + rr);
         }
         wave_sync();
+        SC_PROF(c_merge);
     }
+#if SC_PROF_CHAIN
+    if (w.prof && lane == 0) {
+        atomicAdd(&w.prof[0], c_idle);
+        atomicAdd(&w.prof[1], c_setup);
+        atomicAdd(&w.prof[2], c_eval);
+        atomicAdd(&w.prof[3], c_merge);
+        atomicAdd(&w.prof[4], n_rounds);
+        atomicAdd(&w.prof[5], n_slots);
+        atomicAdd(&w.prof[6], c_deq);
+        atomicAdd(&w.prof[7], c_poll);
+    }
+#endif
 }
 
 }  // namespace
@@ -798,7 +872,7 @@ void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s) {
 }
 
 int launch_chain(const CascadeArgs &a, const WalkArgs &w, int device, hipStream_t s) {
-    const size_t scratch = kWavesPerWg * chain_wave_bytes(w.row_max);
+    const size_t scratch = kWavesPerWg * chain_wave_bytes(w.row_max) + w.n_levels * sizeof(LevelInfo);
     bool lw = model_lds_bytes(a.K, true) + scratch <= 160 * 1024;
     if (const char *e = std::getenv("SC_LDS_WEIGHTS")) lw = std::atoi(e) != 0;  // tuning override
     const size_t lds = model_lds_bytes(a.K, lw) + scratch;
@@ -823,8 +897,9 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, int device, hipStream_
     return grid;
 }
 
-size_t chain_lds_bytes(int K, int row_max) {  // smallest variant
-    return model_lds_bytes(K, false) + kWavesPerWg * chain_wave_bytes(row_max);
+size_t chain_lds_bytes(int K, int row_max, int n_levels) {  // smallest variant
+    return model_lds_bytes(K, false) + kWavesPerWg * chain_wave_bytes(row_max) +
+           n_levels * sizeof(LevelInfo);
 }
 
 size_t cascade_lds_bytes(int K, int strip_max, int band_rows) {  // smallest variant
