@@ -55,7 +55,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
-    ap.add_argument("--batch", type=int, help="frames per GPU per step (config default)")
+    ap.add_argument("--batch", type=int, help="frames per GPU per step (config default; 1 with "
+                    "--shard grid)")
+    ap.add_argument("--shard", default="frames", choices=("frames", "grid"),
+                    help="frames: each rank scans its own frames (C3, weak scaling); grid: every "
+                         "rank scans the same frames, its (level, y) rows only (SURVEY 8e "
+                         "single-frame runs, strong scaling)")
     ap.add_argument("--width", type=int)
     ap.add_argument("--height", type=int)
     ap.add_argument("--levels", type=int)
@@ -64,6 +69,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     a = ap.parse_args()
     c = CONFIGS[a.config]
+    if a.batch is None and a.shard == "grid":
+        a.batch = 1
     for k in ("batch", "width", "height", "levels"):
         if getattr(a, k) is None:
             setattr(a, k, c[k])
@@ -131,13 +138,17 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     W, H, B = args.width, args.height, args.batch
-    # frame sharding: rank r owns frames 1000 + r*B .. (seeds) -- C3 layout
-    start, _ = shard_range(B * world, world, rank)
+    # frame sharding: rank r owns frames 1000 + r*B .. (seeds) -- C3 layout;
+    # grid sharding: every rank holds frames 1000 .. and scans its rows of them
+    grid_shard = args.shard == "grid"
+    start = 0 if grid_shard else shard_range(B * world, world, rank)[0]
     host_frames = synth.make_frames(W, H, B, seed0=1000 + start)
     frames = torch.from_numpy(host_frames).to(f"cuda:{local_rank}")
     params = (sc.ScanParams.pedestrian(n_levels=args.levels) if args.pedestrian
               else sc.ScanParams(n_levels=args.levels))
     det = sc.Detector(args.model, params, device=local_rank)
+    if grid_shard:
+        det.set_shard(rank, world)
     cap = 256 * B
     recs = torch.zeros(cap * sc.RECORD_DTYPE.itemsize, dtype=torch.uint8, device=frames.device)
     counts = torch.zeros(1 + B, dtype=torch.int32, device=frames.device)
@@ -173,11 +184,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     merged = merge_records(gathered["counts"], gathered["recs"],
-                           [shard_range(B * world, world, r)[0] for r in range(world)])
+                           [0 if grid_shard else shard_range(B * world, world, r)[0]
+                            for r in range(world)])
     total_det = len(merged)
 
     if rank == 0:
-        windows = grid * B * args.steps * world
+        windows = grid * B * args.steps * (1 if grid_shard else world)
         value = windows / dt
         # roofline of the dominant kernel (windows): its compulsory bytes per
         # launch = the integral table read once (32 B x (W+1)(H+1) per frame)
@@ -205,17 +217,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if grid_shard else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded %dx%d frames, seeded 10-stage %s cascade, thetas calibrated "
                     "on held-out frames)" % (W, H, "64x128" if args.pedestrian else "40x40"),
-            "config": {"workload": (CONFIGS[args.config]["desc"] + "; frame-sharded, %d frames per "
-                                    "GPU per step") % (W, H, args.levels,
-                                                       params.level_len(args.levels - 1), B),
+            "config": {"workload": (CONFIGS[args.config]["desc"] + (
+                           "; window grid sharded by rows over the GPUs, %d frame(s) per step"
+                           if grid_shard else "; frame-sharded, %d frames per GPU per step"))
+                           % (W, H, args.levels, params.level_len(args.levels - 1), B),
                        "name": args.config,
                        "frames_per_gpu_per_step": B, "grid_windows_per_frame": grid,
-                       "levels": args.levels, "parallelism": "frame-sharded dp%d" % world},
+                       "levels": args.levels,
+                       "parallelism": ("grid-row-sharded x%d" if grid_shard else "frame-sharded dp%d")
+                       % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": ("cascade_kernel" if os.environ.get("SC_FULL_GRID", "0") != "0"

@@ -108,6 +108,15 @@ int sc_detect_batch(sc_detector *d, const uint8_t *const *frames, int n,
 int sc_detect_device(sc_detector *d, const uint8_t *d_frames, int n, int w,
                      int h, int stride_bytes, sc_window *out, int capacity,
                      int *n_out);
+/* Window-grid sharding of every frame over `world` ranks (SURVEY.md 8e:
+ * single-frame 1/2/4/8-GPU runs).  This detector then evaluates only the
+ * (level, y) rows i of the canonical row list (level-major, y ascending)
+ * with i % world == rank; the adaptive-stride x chain never leaves its row
+ * (ObjDetector.cpp:185-217), so the union over ranks of the raw windows is
+ * exactly the unsharded result.  The reference has no multi-device path; the
+ * closest thing is its OpenMP split over levels (ObjDetector.cpp:177).
+ * (rank 0, world 1) restores the whole grid. */
+int sc_detector_set_shard(sc_detector *d, int rank, int world);
 /* Asynchronous form on the detector's stream: device records (unsorted;
  * canonical order = sort by frame, level, y, x) + device counters
  * d_counts[0] = total, d_counts[1+f] = frame f's count.  No host sync. */

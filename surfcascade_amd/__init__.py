@@ -47,7 +47,7 @@ EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_mode
            "sc_extract_patches", "sc_detector_create", "sc_detector_create_from_model",
            "sc_detector_destroy", "sc_detect", "sc_detect_batch", "sc_detect_device",
            "sc_enqueue_device", "sc_synchronize", "sc_detector_stream", "sc_detector_info",
-           "sc_detector_set_debug", "sc_debug_dump", "sc_set_timing", "sc_get_timing",
+           "sc_detector_set_shard", "sc_detector_set_debug", "sc_debug_dump", "sc_set_timing", "sc_get_timing",
            "sc_group_rectangles", "sc_group_detections", "sc_fddb_format",
            "sc_miner_create", "sc_mine",
            "sc_last_error", "sc_version")
@@ -137,6 +137,7 @@ def load_library():
     L.sc_detector_stream.restype = vp
     L.sc_detector_info.argtypes = [vp, i32, P(i64)]
     L.sc_detector_set_debug.argtypes = [vp, i32]
+    L.sc_detector_set_shard.argtypes = [vp, i32, i32]
     L.sc_debug_dump.argtypes = [vp, i32, i32, vp, sz]
     L.sc_set_timing.argtypes = [vp, i32]
     L.sc_get_timing.argtypes = [vp, P(ctypes.c_double), P(i64)]
@@ -404,6 +405,11 @@ class Detector:
 
     def set_debug(self, on=True):
         _check(load_library().sc_detector_set_debug(self._h, int(on)))
+
+    def set_shard(self, rank, world):
+        """Window-grid sharding (sc_detector_set_shard): evaluate only the
+        (level, y) rows i with i % world == rank of every frame."""
+        _check(load_library().sc_detector_set_shard(self._h, int(rank), int(world)))
 
     def dump_integral(self, W, H, frame=0):
         T = np.zeros((H + 1, W + 1, 8), np.float32)

@@ -97,6 +97,7 @@ struct sc_detector {
     DevBuf<int16_t> d_order;      // per stage: weak indices sorted by patch shape
     int chunk_min = 1 << 30;  // one-lane-per-window stages only when n > item buffer
     bool lazy = true;         // chain kernel: only windows the x chain reaches are evaluated
+    int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
     Geometry geo;
     DevBuf<sc::LevelInfo> d_levels;
@@ -289,6 +290,19 @@ void build_geometry(sc_detector *d, int W, int H) {
         ng.levels.push_back(L);
     }
     ng.grid = gb;  // may be 0: no window fits (the reference loop runs 0 times)
+    if (d->shard_world > 1) {
+        // single-frame window-grid sharding: this rank keeps
+        // the (level, y) rows i of the canonical row list with i % world ==
+        // rank -- every rank gets ny/world (+-1) rows of every level, so the
+        // grid windows balance, and spatially clustered work spreads over the
+        // ranks.  The adaptive-stride chain never leaves its row
+        // (ObjDetector.cpp:185-217), so the rows are independent; grid
+        // indices (dumps) stay those of the whole frame.
+        std::vector<int2> mine;
+        for (size_t i = 0; i < ng.rows.size(); i++)
+            if ((int)(i % (size_t)d->shard_world) == d->shard_rank) mine.push_back(ng.rows[i]);
+        ng.rows.swap(mine);
+    }
     {   // cascade tasks: one strip (~72 windows wide at the widest level) of a
         // band of band_rows consecutive grid rows of one level
         const char *e = std::getenv("SC_SUBSTRIPS");  // tuning overrides
@@ -296,6 +310,7 @@ void build_geometry(sc_detector *d, int W, int H) {
                      : std::max(1, (ng.nx_max + sc::kXcds * 72 / 2) / (sc::kXcds * 72));
         const char *eb = std::getenv("SC_BAND_ROWS");
         ng.band_rows = eb ? std::max(1, std::atoi(eb)) : kBandRows;
+        if (d->shard_world > 1) ng.band_rows = 1;  // a rank's rows are not consecutive
         const int nseg = sc::kXcds * ng.n_sub;
         ng.strip_max = std::max(1, (ng.nx_max + nseg - 1) / nseg);
         if (ng.strip_max > 0xffff) throw Error{SC_ERR_INVALID, "strip too wide"};
@@ -1053,6 +1068,18 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value) {
             });
         }
         default: return fail(SC_ERR_INVALID, "unknown info key");
+    }
+    return SC_OK;
+}
+
+int sc_detector_set_shard(sc_detector *d, int rank, int world) {
+    if (!d) return fail(SC_ERR_INVALID, "null detector");
+    if (world < 1 || rank < 0 || rank >= world) return fail(SC_ERR_INVALID, "bad shard rank/world");
+    if (d->miner) return fail(SC_ERR_INVALID, "a miner scans whole images");
+    if (d->shard_rank != rank || d->shard_world != world) {
+        d->shard_rank = rank;
+        d->shard_world = world;
+        d->geo.W = d->geo.H = 0;  // rebuild the row list at the next detect
     }
     return SC_OK;
 }

@@ -1,7 +1,8 @@
 """Frame sharding + detection gather across ranks.
 
 Frames are independent, so a batch shards over ranks with no data-path
-exchange; the only collective is the gather of the raw detection records at
+exchange (C3); a single frame shards by (level, y) rows of its window grid
+(Detector.set_shard, every rank rebuilds the integral table); the only collective is the gather of the raw detection records at
 the end: one all_gather of the per-frame counts and one all_gather of a
 fixed-capacity record buffer (RCCL over xGMI on GPUs, gloo in CPU tests).
 Records (RECORD_DTYPE, 40 B) are unsorted on the device; merge_records()
@@ -19,6 +20,19 @@ def shard_range(n_total: int, world: int, rank: int):
     base, rem = divmod(n_total, world)
     start = rank * base + min(rank, rem)
     return start, base + (1 if rank < rem else 0)
+
+
+def grid_row_owner(layout, step, world):
+    """Owner rank of every (level, y) row under sc_detector_set_shard's rule:
+    row i of the canonical row list (level-major, y ascending) goes to rank
+    i % world.  layout: [(level, l, lh, nx, ny, base)] (oracle.grid_layout).
+    Returns {(level, y): rank}."""
+    own, i = {}, 0
+    for (lv, _l, _lh, _nx, ny, _b) in layout:
+        for r in range(ny):
+            own[(lv, r * step)] = i % world
+            i += 1
+    return own
 
 
 def gather_detections(counts, recs, group=None):

@@ -90,3 +90,71 @@ def test_gloo_gather_equals_single_process(oracle, world):
     ref = merge_records([np.array([len(a)])], [a.view(np.uint8)], [0])
     assert len(ref) > 50
     assert got.tobytes() == ref.tobytes()
+
+
+def _grid_worker(rank, world, port, n_frames, out_q):
+    """Grid sharding: every rank scans the same frames, its own rows only."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as O
+    from surfcascade_amd import RECORD_DTYPE, synth
+    from surfcascade_amd.dist import gather_detections, grid_row_owner, merge_records
+    casc = O.cascade_from_cfg(open(FACE_CFG).read())
+    casc.theta[:] = np.float32(0.45)
+    params = O.Params(n_levels=3)
+    frames = np.stack([synth.make_frame(320, 240, 500 + k) for k in range(n_frames)])
+    layout, step = O.grid_layout(320, 240, params)
+    own = grid_row_owner(layout, step, world)
+    a = _records_for(O, casc, frames, params, 0, np.random.default_rng(rank))
+    a = a[[own[(int(r["level"]), int(r["y"]))] == rank for r in a]]  # this rank's rows
+    cap = 1 << 15
+    buf = np.zeros(cap, RECORD_DTYPE)
+    buf[:len(a)] = a
+    counts = np.zeros(1 + n_frames, np.int32)
+    counts[0] = len(a)
+    gc, gr = gather_detections(torch.from_numpy(counts), torch.from_numpy(buf.view(np.uint8).copy()))
+    merged = merge_records(gc, gr, [0] * world)  # same frames on every rank
+    if rank == 0:
+        out_q.put(merged.tobytes())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_grid_row_owner_partitions_rows(oracle):
+    from surfcascade_amd.dist import grid_row_owner
+    layout, step = oracle.grid_layout(1920, 1080, oracle.Params(n_levels=24))
+    for world in (1, 2, 8):
+        own = grid_row_owner(layout, step, world)
+        assert len(own) == sum(e[4] for e in layout)
+        # grid windows per rank balance to within one row of each level
+        per = np.zeros(world, np.int64)
+        for (lv, _l, _lh, nx, ny, _b) in layout:
+            for r in range(ny):
+                per[own[(lv, r * step)]] += nx
+        assert per.max() - per.min() <= max(e[3] for e in layout) * len(layout)
+
+
+def test_gloo_grid_shard_gather_equals_single_process(oracle):
+    from surfcascade_amd import RECORD_DTYPE
+    from surfcascade_amd.dist import merge_records
+    world, n_frames = 2, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() + 500) % 1000
+    procs = [ctx.Process(target=_grid_worker, args=(r, world, port, n_frames, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = np.frombuffer(q.get(timeout=120), RECORD_DTYPE)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    casc = oracle.cascade_from_cfg(open(FACE_CFG).read())
+    casc.theta[:] = np.float32(0.45)
+    from surfcascade_amd import synth
+    frames = np.stack([synth.make_frame(320, 240, 500 + k) for k in range(n_frames)])
+    a = _records_for(oracle, casc, frames, oracle.Params(n_levels=3), 0, np.random.default_rng(9))
+    ref = merge_records([np.array([len(a)])], [a.view(np.uint8)], [0])
+    assert len(ref) > 20
+    assert got.tobytes() == ref.tobytes()

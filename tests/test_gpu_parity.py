@@ -234,3 +234,38 @@ def test_grouped_detections_match_oracle(sc, oracle, face_cascade):
         assert sc.fddb_format("f%d" % k, a) == oracle.fddb_format("f%d" % k, b)
         n_groups += len(a)
     assert n_groups > 0
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_grid_shards_union_equals_whole(sc, oracle, face_cascade, world):
+    """Single-frame window-grid sharding: the ranks' row sets
+    partition the grid and the union of their raw windows (and visited counts)
+    is the unsharded result, which equals the oracle's."""
+    from surfcascade_amd import synth
+    c = face_cascade
+    theta = np.full(c.n_stages, 0.45, np.float32)  # ~10^4 detections per frame
+    text = synth.write_cfg(synth.cascade_tree(c.n_weak, theta, c.patch_index, c.w, c.bias))
+    frames = np.stack([_frame(1920, 1080, 1000 + k) for k in range(2)])
+    casc_or = oracle.cascade_from_cfg(text)
+    ref, vis = [], 0
+    for k in range(2):
+        r, nv = oracle.detect(oracle.integral(frames[k]), casc_or, oracle.Params(n_levels=24))
+        ref.append(_det_set(r))
+        vis += nv
+    det = sc.Detector(sc.Model.parse(text), sc.ScanParams(n_levels=24))
+    got = [[], []]
+    vsum, nrows = 0, 0
+    for rank in range(world):
+        det.set_shard(rank, world)
+        res = det.detect_batch(frames)
+        for k in range(2):
+            got[k] += _det_set(res[k])
+        vsum += det.info("visited")
+        nrows += det.info("rows")
+    det.set_shard(0, 1)
+    whole = det.detect_batch(frames)
+    assert nrows == det.info("rows")
+    for k in range(2):
+        assert sorted(got[k]) == ref[k] == _det_set(whole[k])
+    assert vsum == vis == det.info("visited")
+    assert sum(len(r) for r in ref) > 100
