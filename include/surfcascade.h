@@ -203,6 +203,27 @@ int sc_group_detections(const sc_det_record *rec, int n, int n_frames,
 int sc_fddb_format(const char *image_name, const sc_scored_rect *r, int n,
                    char *buf, size_t cap, size_t *len);
 
+/* fast_nms (ObjDetector.cpp:318-383), the reference's commented-out
+ * alternative to groupRectangles (:223): greedy suppression of every
+ * rectangle whose (w+1)(h+1)-normalised overlap with the current best
+ * exceeds overlap_th, in the reference's exact tie order (its exchange sort,
+ * :275-288, is reproduced as written: O(n^2)).  out = picked rectangles in
+ * pick order (best score first); SC_ERR_CAPACITY when *n_out > capacity. */
+int sc_fast_nms(const sc_scored_rect *in, int n, double overlap_th,
+                sc_scored_rect *out, int capacity, int *n_out);
+
+/* ---- input side (ObjDetector.cpp:164) -----------------------------------
+ * cv::imread(path, cv::IMREAD_GRAYSCALE) for JPEG files: baseline,
+ * extended-sequential and progressive Huffman JPEG, 8-bit, 1 or 3 components
+ * (luma, as libjpeg's JCS_GRAYSCALE output: JDCT_ISLOW inverse DCT).  Writes
+ * a w x h plane with row stride w.  *w / *h are set even when the buffer is
+ * too small (SC_ERR_CAPACITY), so a NULL / 0 call sizes the buffer.
+ * SC_ERR_PARSE: not a JPEG, or an unsupported coding process. */
+int sc_decode_jpeg_gray(const uint8_t *data, size_t len, uint8_t *out,
+                        size_t cap, int *w, int *h);
+int sc_imread_gray(const char *path, uint8_t *out, size_t cap, int *w,
+                   int *h);
+
 const char *sc_last_error(void);
 const char *sc_version(void);
 

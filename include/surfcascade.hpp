@@ -149,6 +149,39 @@ inline void groupRectangles(std::vector<Rect> &rectList, std::vector<int> &weigh
     weights.assign(n, 0);
 }
 
+// fast_nms(rects, scores, overlap_th) (ObjDetector.cpp:318-383): rects and
+// scores become the picked windows, best first.
+inline void fast_nms(std::vector<Rect> &rects, std::vector<double> &scores, double overlap_th) {
+    if (scores.size() != rects.size()) throw Error(SC_ERR_INVALID, "scores size");
+    std::vector<sc_scored_rect> in(rects.size()), out(rects.size() + 1);
+    for (size_t i = 0; i < rects.size(); i++)
+        in[i] = {rects[i].x, rects[i].y, rects[i].width, rects[i].height, scores[i]};
+    int n = 0;
+    check(sc_fast_nms(in.data(), (int)in.size(), overlap_th, out.data(), (int)out.size(), &n));
+    rects.clear();
+    scores.clear();
+    for (int i = 0; i < n; i++) {
+        rects.push_back({out[i].x, out[i].y, out[i].width, out[i].height});
+        scores.push_back(out[i].score);
+    }
+}
+
+// A gray image as cv::imread(path, cv::IMREAD_GRAYSCALE) returns it for a
+// JPEG file (ObjDetector.cpp:164): continuous rows, stride = width.
+struct GrayImage {
+    int width = 0, height = 0;
+    std::vector<uint8_t> data;
+    bool empty() const { return data.empty(); }
+};
+inline GrayImage imread_gray(const std::string &path) {
+    GrayImage g;
+    int rc = sc_imread_gray(path.c_str(), nullptr, 0, &g.width, &g.height);
+    if (rc != SC_ERR_CAPACITY) check(rc);
+    g.data.resize((size_t)g.width * g.height);
+    check(sc_imread_gray(path.c_str(), g.data.data(), g.data.size(), &g.width, &g.height));
+    return g;
+}
+
 // The per-image block of the reference's output file (ObjDetector.cpp:228-231).
 inline std::string FddbBlock(const std::string &name, const std::vector<Rect> &wins,
                              const std::vector<double> &scores) {

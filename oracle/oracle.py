@@ -121,6 +121,61 @@ def group_rectangles(rects, group_threshold=2, eps=0.2):
     return out[:n].copy()
 
 
+def fast_nms(rects, overlap_th=0.7):
+    """fast_nms restated line by line in Python (ObjDetector.cpp:275-383):
+    exchange sort ascending by score (:275-288), pick the last, suppress by
+    float inverse +1 area (:334-365), compact with sort_stable (:290-313).
+    rects: RECT_DTYPE; returns the picked rows in pick order."""
+    r = np.ascontiguousarray(rects, RECT_DTYPE)
+    n = len(r)
+    sc = [float(v) for v in r["score"]]
+    idx = list(range(n))
+    for i in range(n):
+        for j in range(i + 1, n):
+            ti, tj = idx[i], idx[j]
+            if sc[tj] < sc[ti]:
+                idx[i], idx[j] = tj, ti
+    inv = [0.0] * n
+    for i in range(n):
+        w, h = int(r["width"][idx[i]]), int(r["height"][idx[i]])
+        inv[idx[i]] = np.float32(1.0) / np.float32((w + 1) * (h + 1))
+
+    def sort_stable(cnt):
+        i = j = 0
+        while i < cnt:
+            if idx[i] == -1:
+                if j < i + 1:
+                    j = i + 1
+                while j < cnt:
+                    if idx[j] == -1:
+                        j += 1
+                    else:
+                        idx[i], idx[j] = idx[j], -1
+                        j += 1
+                        break
+                if j == cnt:
+                    return i
+            i += 1
+        return i
+
+    pick, count = [], n
+    X, Y, W, H = (r[k].astype(np.int64) for k in ("x", "y", "width", "height"))
+    while count > 0:
+        last = idx[count - 1]
+        pick.append(last)
+        x0, y0, x1, y1 = X[last], Y[last], X[last] + W[last], Y[last] + H[last]
+        idx[count - 1] = -1
+        for i in range(count - 2, -1, -1):
+            q = idx[i]
+            tx0, ty0 = max(x0, X[q]), max(y0, Y[q])
+            tx1, ty1 = min(x1, X[q] + W[q]), min(y1, Y[q] + H[q])
+            tx0, ty0 = tx1 - tx0 + 1, ty1 - ty0 + 1
+            if tx0 > 0 and ty0 > 0 and float(np.float32(tx0 * ty0) * inv[q]) > overlap_th:
+                idx[i] = -1
+        count = sort_stable(count)
+    return r[pick].copy()
+
+
 def fddb_format(name, rects):
     r = np.ascontiguousarray(rects, RECT_DTYPE)
     data = r.ctypes.data if len(r) else None

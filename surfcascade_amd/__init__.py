@@ -49,7 +49,7 @@ EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_mode
            "sc_enqueue_device", "sc_synchronize", "sc_detector_stream", "sc_detector_info",
            "sc_detector_set_shard", "sc_detector_set_debug", "sc_debug_dump", "sc_set_timing", "sc_get_timing",
            "sc_group_rectangles", "sc_group_detections", "sc_fddb_format",
-           "sc_miner_create", "sc_mine",
+           "sc_miner_create", "sc_mine", "sc_fast_nms", "sc_decode_jpeg_gray", "sc_imread_gray",
            "sc_last_error", "sc_version")
 
 
@@ -146,6 +146,9 @@ def load_library():
     L.sc_group_rectangles.argtypes = [vp, i32, i32, ctypes.c_double, vp, i32, P(i32)]
     L.sc_group_detections.argtypes = [vp, i32, i32, i32, ctypes.c_double, vp, i32, vp, P(i32)]
     L.sc_fddb_format.argtypes = [ctypes.c_char_p, vp, i32, ctypes.c_char_p, sz, P(sz)]
+    L.sc_fast_nms.argtypes = [vp, i32, ctypes.c_double, vp, i32, P(i32)]
+    L.sc_decode_jpeg_gray.argtypes = [vp, sz, vp, sz, P(i32), P(i32)]
+    L.sc_imread_gray.argtypes = [ctypes.c_char_p, vp, sz, P(i32), P(i32)]
     _lib = L
     return L
 
@@ -219,6 +222,46 @@ def fddb_format(name, rects):
     buf = ctypes.create_string_buffer(need.value + 1)
     _check(L.sc_fddb_format(name.encode(), data, len(r), buf, need.value + 1, ctypes.byref(need)))
     return buf.value.decode()
+
+
+def fast_nms(rects, overlap_th=0.7):
+    """fast_nms (ObjDetector.cpp:318-383; the reference calls it with 0.7 in the
+    commented-out line :223): the picked rectangles in pick order."""
+    L = load_library()
+    r = _as_rects(rects)
+    out = np.zeros(max(len(r), 1), RECT_DTYPE)
+    n = ctypes.c_int32(0)
+    _check(L.sc_fast_nms(r.ctypes.data if len(r) else None, len(r), float(overlap_th),
+                         out.ctypes.data, len(out), ctypes.byref(n)))
+    return out[:n.value].copy()
+
+
+# ---------------------------------------------------------------------------
+# input side (ObjDetector.cpp:164): cv::imread(path, IMREAD_GRAYSCALE) for JPEG
+# ---------------------------------------------------------------------------
+
+def _decode(call):
+    w, h = ctypes.c_int32(0), ctypes.c_int32(0)
+    rc = call(None, 0, ctypes.byref(w), ctypes.byref(h))
+    if rc != -6:
+        _check(rc)
+    img = np.zeros((h.value, w.value), np.uint8)
+    _check(call(img.ctypes.data, img.nbytes, ctypes.byref(w), ctypes.byref(h)))
+    return img
+
+
+def decode_jpeg_gray(data: bytes):
+    """JPEG bytes -> (H, W) uint8 luma plane (libjpeg JCS_GRAYSCALE, JDCT_ISLOW)."""
+    L = load_library()
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    return _decode(lambda o, c, w, h: L.sc_decode_jpeg_gray(buf, len(data), o, c, w, h))
+
+
+def imread_gray(path):
+    """cv::imread(path, cv::IMREAD_GRAYSCALE) for a JPEG file."""
+    L = load_library()
+    p = os.fsencode(path)
+    return _decode(lambda o, c, w, h: L.sc_imread_gray(p, o, c, w, h))
 
 
 # ---------------------------------------------------------------------------

@@ -15,12 +15,14 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <iterator>
 #include <sstream>
 #include <string>
 #include <vector>
 
 #include "sc_kernels.hpp"
 #include "sc_group.hpp"
+#include "sc_jpeg.hpp"
 #include "sc_model.hpp"
 #include "surfcascade.h"
 
@@ -931,6 +933,50 @@ int sc_fddb_format(const char *name, const sc_scored_rect *r, int n, char *buf, 
         if (!buf || cap <= s.size()) throw Error{SC_ERR_CAPACITY, "buffer too small"};
         std::memcpy(buf, s.c_str(), s.size() + 1);
         return SC_OK;
+    });
+}
+
+int sc_fast_nms(const sc_scored_rect *in, int n, double overlap_th, sc_scored_rect *out,
+                int capacity, int *n_out) {
+    return guarded([&] {
+        if ((n > 0 && !in) || n < 0 || !n_out || capacity < 0 || (capacity > 0 && !out))
+            throw Error{SC_ERR_INVALID, "bad arguments"};
+        const std::vector<sc_scored_rect> r = sc::fast_nms(in, n, overlap_th);
+        *n_out = (int)r.size();
+        std::copy(r.begin(), r.begin() + std::min<size_t>(r.size(), (size_t)capacity), out);
+        if ((int)r.size() > capacity) throw Error{SC_ERR_CAPACITY, "output capacity too small"};
+        return SC_OK;
+    });
+}
+
+namespace {
+int decode_into(const uint8_t *data, size_t len, uint8_t *out, size_t cap, int *w, int *h) {
+    if (!data || !w || !h) throw Error{SC_ERR_INVALID, "null argument"};
+    std::string err;
+    int W = 0, H = 0;
+    if (sc::jpeg_gray(data, len, nullptr, &W, &H, &err) != 0) throw Error{SC_ERR_PARSE, err};
+    *w = W;
+    *h = H;
+    if (!out || cap < (size_t)W * H)
+        throw Error{SC_ERR_CAPACITY, "gray plane needs " + std::to_string((size_t)W * H) + " bytes"};
+    std::vector<uint8_t> img;
+    if (sc::jpeg_gray(data, len, &img, &W, &H, &err) != 0) throw Error{SC_ERR_PARSE, err};
+    std::memcpy(out, img.data(), img.size());
+    return SC_OK;
+}
+}  // namespace
+
+int sc_decode_jpeg_gray(const uint8_t *data, size_t len, uint8_t *out, size_t cap, int *w, int *h) {
+    return guarded([&] { return decode_into(data, len, out, cap, w, h); });
+}
+
+int sc_imread_gray(const char *path, uint8_t *out, size_t cap, int *w, int *h) {
+    return guarded([&] {
+        if (!path) throw Error{SC_ERR_INVALID, "null path"};
+        std::ifstream f(path, std::ios::binary);
+        if (!f) throw Error{SC_ERR_IO, std::string("cannot open ") + path};
+        std::vector<uint8_t> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        return decode_into(buf.data(), buf.size(), out, cap, w, h);
     });
 }
 

@@ -139,4 +139,71 @@ std::string fddb_block(const char *name, const sc_scored_rect *r, int n) {
     return s;
 }
 
+// fast_nms (ObjDetector.cpp:318-383; commented out at :223, the reference's
+// alternative to groupRectangles).  Followed literally, including its
+// quirks: sort_idx (:275-288) is an exchange sort ASCENDING by score (despite
+// its comment) whose tie order depends on the swaps, so it is simulated as
+// written, O(n^2); the pick is the LAST remaining index (the best score);
+// overlap uses +1 areas, a float inverse area 1.0f/((w+1)*(h+1)) and the
+// int*float product compared with the double threshold; suppressed entries
+// are compacted by sort_stable (:290-313).
+std::vector<sc_scored_rect> fast_nms(const sc_scored_rect *in, int n, double overlap_th) {
+    std::vector<int> idx(std::max(n, 0));
+    std::vector<float> inv(std::max(n, 0));
+    std::iota(idx.begin(), idx.end(), 0);
+    for (int i = 0; i < n; i++)  // sort_idx
+        for (int j = i + 1; j < n; j++) {
+            const int ti = idx[i], tj = idx[j];
+            if (in[tj].score < in[ti].score) {
+                idx[i] = tj;
+                idx[j] = ti;
+            }
+        }
+    for (int i = 0; i < n; i++) {
+        const sc_scored_rect &r = in[idx[i]];
+        inv[idx[i]] = 1.0f / (float)((r.width + 1) * (r.height + 1));
+    }
+    auto sort_stable = [&](int cnt) {  // :290-313, returns the new count
+        int i = 0, j = 0;
+        while (i < cnt) {
+            if (idx[i] == -1) {
+                if (j < i + 1) j = i + 1;
+                while (j < cnt) {
+                    if (idx[j] == -1) {
+                        ++j;
+                    } else {
+                        idx[i] = idx[j];
+                        idx[j] = -1;
+                        j++;
+                        break;
+                    }
+                }
+                if (j == cnt) return i;
+            }
+            ++i;
+        }
+        return i;
+    };
+    std::vector<sc_scored_rect> picked;
+    int count = n;
+    while (count > 0) {
+        const int tmp = count - 1, last = idx[tmp];
+        picked.push_back(in[last]);
+        const int x0 = in[last].x, y0 = in[last].y;
+        const int x1 = in[last].x + in[last].width, y1 = in[last].y + in[last].height;
+        idx[tmp] = -1;
+        for (int i = tmp - 1; i != -1; i--) {
+            const sc_scored_rect &r = in[idx[i]];
+            int tx0 = std::max(x0, r.x), ty0 = std::max(y0, r.y);
+            const int tx1 = std::min(x1, r.x + r.width), ty1 = std::min(y1, r.y + r.height);
+            tx0 = tx1 - tx0 + 1;
+            ty0 = ty1 - ty0 + 1;
+            if (tx0 > 0 && ty0 > 0 && (double)((float)(tx0 * ty0) * inv[idx[i]]) > overlap_th)
+                idx[i] = -1;
+        }
+        count = sort_stable(count);
+    }
+    return picked;
+}
+
 }  // namespace sc

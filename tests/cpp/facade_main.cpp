@@ -26,6 +26,16 @@ int main(int argc, char **argv) {
                     cascade.stage_classifiers[s].theta, idx[s].size(), idx[s][0]);
     surfcascade::Model out(argv[2]);
     if (out.Save(cascade) != EXIT_SUCCESS) return 1;
+    if (argc == 4) {  // facade_main MODEL.cfg OUT.cfg IMAGE.jpg: imread + fast_nms (host only)
+        const surfcascade::GrayImage g = surfcascade::imread_gray(argv[3]);
+        unsigned long sum = 0;
+        for (uint8_t v : g.data) sum += v;
+        std::printf("image %d %d %lu\n", g.width, g.height, sum);
+        std::vector<surfcascade::Rect> r = {{0, 0, 40, 40}, {2, 2, 40, 40}, {100, 100, 40, 40}};
+        std::vector<double> s = {0.7, 0.9, 0.8};
+        surfcascade::fast_nms(r, s, 0.7);
+        for (size_t i = 0; i < r.size(); i++) std::printf("nms %d %d %.3f\n", r[i].x, r[i].y, s[i]);
+    }
     if (argc >= 6) {
         std::ifstream f(argv[3], std::ios::binary);
         std::vector<uint8_t> img((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());

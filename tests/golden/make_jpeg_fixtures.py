@@ -1,0 +1,53 @@
+"""Writes the JPEG golden fixtures of tests/test_jpeg.py (run from the repo root):
+small JPEG files encoded by Pillow's libjpeg-turbo, and the gray plane that
+decoder returns for each in JCS_GRAYSCALE mode (Image.draft('L'), the luma
+component as cv::imread(..., IMREAD_GRAYSCALE) asks libjpeg for it,
+ObjDetector.cpp:164).  The fixtures let the parity test run where Pillow is
+absent; tests/test_jpeg.py also compares against Pillow live when it is present."""
+import io
+import os
+
+import numpy as np
+from PIL import Image
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def scene(h, w, seed):
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:h, 0:w]
+    base = 128 + 60 * np.sin(x / 7.0) * np.cos(y / 11.0)
+    rgb = np.stack([base, base * 0.8 + 30, 255 - base], -1) + rng.normal(0, 12, (h, w, 3))
+    rgb[h // 4: h // 2, w // 3: w // 2] = (250, 20, 40)
+    return np.clip(rgb, 0, 255).astype(np.uint8)
+
+
+def gray_of(data):
+    im = Image.open(io.BytesIO(data))
+    im.draft("L", im.size)
+    assert im.mode == "L"
+    return np.asarray(im)
+
+
+CASES = [  # name, (h, w), seed, mode, save kwargs
+    ("base420_q75", (37, 53), 1, "RGB", dict(quality=75, subsampling=2)),
+    ("prog444_q90", (48, 64), 2, "RGB", dict(quality=90, subsampling=0, progressive=True)),
+    ("gray_q60_opt", (23, 17), 3, "L", dict(quality=60, optimize=True)),
+    ("prog420_q50", (61, 45), 4, "RGB", dict(quality=50, subsampling=2, progressive=True)),
+]
+
+
+def main():
+    for name, (h, w), seed, mode, kw in CASES:
+        img = scene(h, w, seed)
+        im = Image.fromarray(img if mode == "RGB" else img[..., 0], mode)
+        b = io.BytesIO()
+        im.save(b, "JPEG", **kw)
+        data = b.getvalue()
+        with open(os.path.join(HERE, name + ".jpg"), "wb") as f:
+            f.write(data)
+        np.save(os.path.join(HERE, name + ".gray.npy"), gray_of(data))
+
+
+if __name__ == "__main__":
+    main()

@@ -61,3 +61,16 @@ def test_facade_detect_matches_oracle(facade_bin, tmp_path, oracle):
     lines = lines[:-1]
     block = "\n".join(lines[k + 1 + nd:]) + "\n"
     assert block == oracle.fddb_format("frame", oracle.group_rectangles(sc._as_rects(ref)))
+
+
+def test_facade_imread_and_fast_nms(facade_bin, tmp_path):
+    import glob
+    from conftest import GOLDEN
+    f = sorted(glob.glob(os.path.join(GOLDEN, "*.jpg")))[0]
+    exp = np.load(f[:-4] + ".gray.npy")
+    r = subprocess.run([facade_bin, FACE_CFG, str(tmp_path / "m.cfg"), f], capture_output=True,
+                       text=True)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith(("image", "nms"))]
+    assert lines[0] == "image %d %d %d" % (exp.shape[1], exp.shape[0], int(exp.sum()))
+    assert lines[1:] == ["nms 2 2 0.900", "nms 100 100 0.800"]

@@ -269,3 +269,18 @@ def test_grid_shards_union_equals_whole(sc, oracle, face_cascade, world):
         assert sorted(got[k]) == ref[k] == _det_set(whole[k])
     assert vsum == vis == det.info("visited")
     assert sum(len(r) for r in ref) > 100
+
+
+def test_jpeg_to_detections(sc, oracle, face_cascade):
+    """imread(IMREAD_GRAYSCALE) -> detect, the reference's per-image sequence
+    (ObjDetector.cpp:164-220), against the oracle on the same decoded plane."""
+    import io
+    PIL = pytest.importorskip("PIL.Image")
+    from surfcascade_amd import synth
+    g = synth.make_frame(640, 480, 77)
+    b = io.BytesIO()
+    PIL.fromarray(np.stack([g, g // 2, 255 - g], -1), "RGB").save(b, "JPEG", quality=90)
+    img = sc.decode_jpeg_gray(b.getvalue())
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=4))
+    ref, _ = oracle.detect(oracle.integral(img), face_cascade, oracle.Params(n_levels=4))
+    assert _det_set(det.detect(img)) == _det_set(ref)
