@@ -97,6 +97,7 @@ struct sc_detector {
     DevBuf<float> d_theta;
     DevBuf<int> d_stage_off;
     DevBuf<int16_t> d_order;      // per stage: weak indices sorted by patch shape
+    DevBuf<int4> d_rects;         // per weak: template rect record (sc::InlinePatch)
     int chunk_min = 1 << 30;  // one-lane-per-window stages only when n > item buffer
     bool lazy = true;         // chain kernel: only windows the x chain reaches are evaluated
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
@@ -151,6 +152,7 @@ struct sc_detector {
         }
         for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
         d_w.release(); d_bias.release(); d_theta.release(); d_stage_off.release(); d_order.release();
+        d_rects.release();
         d_levels.release(); d_rows.release(); d_proj.release(); d_tasks.release();
         d_proj_all.release(); d_mine_cnt.release(); d_mine_off.release(); d_mine_win.release();
         d_feat.release();
@@ -220,6 +222,14 @@ void build_geometry(sc_detector *d, int W, int H) {
         t.frame4 = (long long)(H + 1) * t.rowp;
         if ((long long)(H + 1) * t.rowp > (1ll << 28))  // byte offsets within a frame table: u32
             throw Error{SC_ERR_INVALID, "frame too large for 32-bit table offsets"};
+        // x / ph as umulhi(x, ceil(2^32/ph)) in the chain kernel's per-item
+        // projection: exact for every column a patch corner can take
+        t.phm = t.ph > 1 ? (unsigned)((0x100000000ull + (unsigned)t.ph - 1) / (unsigned)t.ph) : 0u;
+        bool exact = t.ph > 1;
+        for (unsigned x = 0; exact && x <= (unsigned)(W + 2 * t.ph); x++)
+            exact = (unsigned)(((unsigned long long)x * t.phm) >> 32) == x / (unsigned)t.ph;
+        if (!exact && d->lazy)
+            throw Error{SC_ERR_INVALID, "phase-plane count unsupported by the chain kernel"};
     }
     const sc::TableGeom &tg = ng.tg;
     // cell of column cx relative to the window origin, for windows of parity
@@ -234,6 +244,7 @@ void build_geometry(sc_detector *d, int W, int H) {
         L.lh = L.l * p.aspect_h;
         L.grid_base = gb;
         L.thr = (float)(L.l * L.lh) * p.prefilter_k;
+        L.scale = (float)L.l / (float)p.tmpl_w;  // ProjectPatches (DenseSURFFeatureExtractor.cpp:463)
         if (L.l >= 1 && L.l <= W && L.lh <= H) {
             L.nx = (W - L.l) / ng.step + 1;
             L.ny = (H - L.lh) / ng.step + 1;
@@ -248,7 +259,7 @@ void build_geometry(sc_detector *d, int W, int H) {
         }
         // ProjectPatches (DenseSURFFeatureExtractor.cpp:459-484) + cell split
         // (GetRectsFromPatch :360-377) for every fitted patch at this level.
-        const float scale = (float)L.l / (float)p.tmpl_w;
+        const float scale = L.scale;
         auto project = [&](const int32_t *r, int par) {
             int px = (int)((float)r[0] * scale), py = (int)((float)r[1] * scale), pw, ph;
             if (r[2] >= r[3]) {
@@ -430,6 +441,20 @@ void upload_model(sc_detector *d) {
         for (size_t j = 0; j < ks.size(); j++) order[off[s] + j] = (int16_t)ks[j];
     }
     if (d->K > 32767) throw Error{SC_ERR_MODEL, "more than 32767 weak classifiers"};
+    // template rect records for the chain kernel's per-item projection
+    // (sc::InlinePatch): ProjectPatches scales ph for square / wide rects and
+    // pw for tall ones (DenseSURFFeatureExtractor.cpp:466-478), then
+    // GetRectsFromPatch splits square rects 2x2 and the others 1x4 / 4x1
+    std::vector<int4> rects(std::max(d->K, 1), make_int4(0, 0, 0, 0));
+    for (int k = 0; k < d->K; k++) {
+        const int32_t *r = &d->patch_rects[4 * k];
+        if (r[2] <= 0 || r[3] <= 0) throw Error{SC_ERR_MODEL, "empty template patch"};
+        const bool wide = r[2] >= r[3];
+        const int ratio = wide ? r[2] / r[3] : r[3] / r[2];
+        if (ratio != 1 && ratio != 4)  // the kernels' cell grids: 2x2, 1x4, 4x1
+            throw Error{SC_ERR_MODEL, "template patch is not 2x2, 1x4 or 4x1 cells"};
+        rects[k] = make_int4(r[0], r[1], wide ? r[3] : r[2], ratio == 1 ? 0 : (wide ? 2 : 1));
+    }
     if (const char *e = std::getenv("SC_CHUNK_MIN")) d->chunk_min = std::max(1, std::atoi(e));
     if (const char *e = std::getenv("SC_FULL_GRID")) d->lazy = std::atoi(e) == 0;  // A/B, dumps
     if (d->miner) d->lazy = false;  // FillNegSamples evaluates every window
@@ -443,6 +468,8 @@ void upload_model(sc_detector *d) {
     HIPCHK(hipMemcpy(d->d_stage_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice));
     d->d_order.ensure(order.size());
     HIPCHK(hipMemcpy(d->d_order.p, order.data(), order.size() * 2, hipMemcpyHostToDevice));
+    d->d_rects.ensure(rects.size());
+    HIPCHK(hipMemcpy(d->d_rects.p, rects.data(), rects.size() * sizeof(int4), hipMemcpyHostToDevice));
 }
 
 void check_params(const sc_scan_params &p) {
@@ -540,6 +567,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     ca.g = g.tg;
     ca.tasks = d->d_tasks.p;
     ca.proj = d->d_proj.p;
+    ca.rects = d->d_rects.p;
     ca.w = reinterpret_cast<const float4 *>(d->d_w.p);
     ca.bias = d->d_bias.p;
     ca.theta = d->d_theta.p;

@@ -19,9 +19,6 @@
 #ifndef SC_LOAD_BARRIER  // 1: every corner load issued before the box sums
 #define SC_LOAD_BARRIER 1
 #endif
-#ifndef SC_HALF_BARRIER  // 1: load the second channel half after the first is consumed
-#define SC_HALF_BARRIER 0
-#endif
 
 namespace sc {
 
@@ -33,18 +30,6 @@ __device__ __forceinline__ float4 box4(float4 tl, float4 br, float4 tr, float4 b
     r.z = (tl.z + br.z) - (tr.z + bl.z);
     r.w = (tl.w + br.w) - (tr.w + bl.w);
     return r;
-}
-
-// c_k = (q0+q1)+(q2+q3); SS = (((eps + c0) + c1) ...) + c7   (:427-433)
-__device__ __forceinline__ float ss_hadd(const float (&f)[32]) {
-    float ss = FLT_EPSILON;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        float q0 = f[4 * k] * f[4 * k], q1 = f[4 * k + 1] * f[4 * k + 1];
-        float q2 = f[4 * k + 2] * f[4 * k + 2], q3 = f[4 * k + 3] * f[4 * k + 3];
-        ss = ss + ((q0 + q1) + (q2 + q3));
-    }
-    return ss;
 }
 
 // A window's view of the table: uniform base (SGPRs) + the lane's 32-bit
@@ -63,72 +48,6 @@ struct TabView {
     }
 };
 
-// The 32 box sums of one projected patch: corners deduplicated on the
-// (GW+1) x (GH+1) corner grid; cell index = row*GW + col (GetRectsFromPatch).
-// All 2*(GW+1)*(GH+1) corner loads are issued before any is consumed (a
-// scheduling barrier keeps the compiler from interleaving them with the
-// math, which would serialise memory round trips within the item).
-template <int GW, int GH>
-__device__ __forceinline__ void patch_features(const TabView &T, const ProjPatch &pj,
-                                               int half_off, float (&f)[32]) {
-#if !SC_LOAD_BARRIER  // A/B: rows loaded as they are consumed (compiler schedules)
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const int ho = h * half_off;
-        float4 prev[GW + 1], cur[GW + 1];
-#pragma unroll
-        for (int c = 0; c <= GW; c++) prev[c] = T.at(ho + pj.row0 + pj.col[c]);
-#pragma unroll
-        for (int r = 0; r < GH; r++) {
-            const int ro = ho + pj.row0 + (r + 1) * pj.rowstep;
-#pragma unroll
-            for (int c = 0; c <= GW; c++) cur[c] = T.at(ro + pj.col[c]);
-#pragma unroll
-            for (int c = 0; c < GW; c++) {
-                const float4 v = box4(prev[c], cur[c + 1], prev[c + 1], cur[c]);
-                const int o = 8 * (r * GW + c) + 4 * h;
-                f[o + 0] = v.x;
-                f[o + 1] = v.y;
-                f[o + 2] = v.z;
-                f[o + 3] = v.w;
-            }
-#pragma unroll
-            for (int c = 0; c <= GW; c++) prev[c] = cur[c];
-        }
-    }
-    return;
-#endif
-    float4 cn[2][GH + 1][GW + 1];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-#pragma unroll
-        for (int r = 0; r <= GH; r++) {
-            const int ro = h * half_off + pj.row0 + r * pj.rowstep;
-#pragma unroll
-            for (int c = 0; c <= GW; c++) cn[h][r][c] = T.at(ro + pj.col[c]);
-        }
-#if SC_HALF_BARRIER
-        __builtin_amdgcn_sched_barrier(0);
-#endif
-    }
-#if !SC_HALF_BARRIER
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-#pragma unroll
-    for (int h = 0; h < 2; h++)
-#pragma unroll
-        for (int r = 0; r < GH; r++)
-#pragma unroll
-            for (int c = 0; c < GW; c++) {
-                const float4 v = box4(cn[h][r][c], cn[h][r + 1][c + 1], cn[h][r][c + 1], cn[h][r + 1][c]);
-                const int o = 8 * (r * GW + c) + 4 * h;
-                f[o + 0] = v.x;
-                f[o + 1] = v.y;
-                f[o + 2] = v.z;
-                f[o + 3] = v.w;
-            }
-}
-
 // A ProjPatch as two 16-B loads issued together (the compiler would
 // otherwise fetch col[] only after branching on shape: a second round trip).
 __device__ __forceinline__ ProjPatch load_proj(const ProjPatch *p) {
@@ -146,37 +65,110 @@ __device__ __forceinline__ ProjPatch load_proj(const ProjPatch *p) {
     return r;
 }
 
-// CalcFeature + Normalize (DenseSURFFeatureExtractor.cpp:379-457) of one
-// projected patch; T views the window's origin cell (half 0).
-__device__ __forceinline__ void descriptor(const TabView &T, int half_off, const ProjPatch &pj,
-                                           float (&f)[32]) {
-    if (pj.shape == 0) patch_features<2, 2>(T, pj, half_off, f);
-    else if (pj.shape == 1) patch_features<1, 4>(T, pj, half_off, f);
-    else patch_features<4, 1>(T, pj, half_off, f);
-    // Normalize (:417-457): clip at sqrt(SS)*theta, renormalise by 1/sqrt(SS2)
+// The 32 features are kept as 16 float pairs, in the order f[2j], f[2j+1]
+// (f index = 8*cell + 4*half + channel): the box sums, the squares, the clip
+// output, the final scale and the LR products then stay in aligned register
+// pairs and issue as v_pk_* (2 lanes of f32 per instruction, each lane's op
+// the reference's own, round-to-nearest) with no re-pairing moves.  Every
+// value and every addition order is the reference's.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// The 32 box sums of one projected patch (CalcFeature :379-415): corners
+// deduplicated on the (GW+1) x (GH+1) corner grid; cell index = row*GW + col
+// (GetRectsFromPatch).  All 2*(GW+1)*(GH+1) corner loads are issued before
+// any is consumed (a scheduling barrier keeps the compiler from interleaving
+// them with the math, which would serialise memory round trips within the
+// item).  P: ProjPatch (host-projected table) or InlinePatch (projected here).
+template <int GW, int GH, class P>
+__device__ __forceinline__ void patch_features2(const TabView &T, const P &pj, int half_off,
+                                                f2 (&fp)[16]) {
+    int col[GW + 1];
+#pragma unroll
+    for (int c = 0; c <= GW; c++) col[c] = pj.colq(c);
+    float4 cn[2][GH + 1][GW + 1];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+#pragma unroll
+        for (int r = 0; r <= GH; r++) {
+            const int ro = h * half_off + pj.row0 + r * pj.rowstep;
+#pragma unroll
+            for (int c = 0; c <= GW; c++) cn[h][r][c] = T.at(ro + col[c]);
+        }
+    }
+#if SC_LOAD_BARRIER
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int r = 0; r < GH; r++)
+#pragma unroll
+            for (int c = 0; c < GW; c++) {
+                // (TL + BR) - (TR + BL), :385-412
+                const float4 tl = cn[h][r][c], br = cn[h][r + 1][c + 1];
+                const float4 tr = cn[h][r][c + 1], bl = cn[h][r + 1][c];
+                const int o = 4 * (r * GW + c) + 2 * h;
+                fp[o] = (f2{tl.x, tl.y} + f2{br.x, br.y}) - (f2{tr.x, tr.y} + f2{bl.x, bl.y});
+                fp[o + 1] = (f2{tl.z, tl.w} + f2{br.z, br.w}) - (f2{tr.z, tr.w} + f2{bl.z, bl.w});
+            }
+}
+
+// c_k = (q0+q1)+(q2+q3) of f[4k..4k+3] = fp[2k], fp[2k+1];
+// SS = (((eps + c0) + c1) ...) + c7   (:427-433)
+__device__ __forceinline__ float ss_hadd2(const f2 (&fp)[16]) {
+    float ss = FLT_EPSILON;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const f2 a = fp[2 * k] * fp[2 * k], b = fp[2 * k + 1] * fp[2 * k + 1];
+        ss = ss + ((a.x + a.y) + (b.x + b.y));
+    }
+    return ss;
+}
+
+// CalcFeature + Normalize (:379-457) of one projected patch.
+template <class P>
+__device__ __forceinline__ void descriptor2(const TabView &T, int half_off, const P &pj, f2 (&fp)[16]) {
+    if (pj.shape == 0) patch_features2<2, 2>(T, pj, half_off, fp);
+    else if (pj.shape == 1) patch_features2<1, 4>(T, pj, half_off, fp);
+    else patch_features2<4, 1>(T, pj, half_off, fp);
     const float theta = 0.35355338f;  // 2/sqrt(32.f) (.h:36)
-    const float t = sqrtf(ss_hadd(f)) * theta, nt = -t;
+    const float t = sqrtf(ss_hadd2(fp)) * theta, nt = -t;
     // _mm_max_ps(_mm_min_ps(f, t), -t) as one v_med3_f32: identical bits here
     // because f is a finite box sum (never NaN, never -0) and t > 0 (SS >= eps)
 #pragma unroll
-    for (int i = 0; i < 32; i++) f[i] = __builtin_amdgcn_fmed3f(f[i], nt, t);
-    const float r = 1.0f / sqrtf(ss_hadd(f));
+    for (int j = 0; j < 16; j++) {
+        fp[j].x = __builtin_amdgcn_fmed3f(fp[j].x, nt, t);
+        fp[j].y = __builtin_amdgcn_fmed3f(fp[j].y, nt, t);
+    }
+    const float r = 1.0f / sqrtf(ss_hadd2(fp));
 #pragma unroll
-    for (int i = 0; i < 32; i++) f[i] = f[i] * r;
+    for (int j = 0; j < 16; j++) fp[j] = fp[j] * f2{r, r};
 }
 
-// LogisticRegression::Predict (LogisticRegression.cpp:46-68); w4 = w[0..35].
-__device__ __forceinline__ float lr_predict(const float (&f)[32], const float4 *w4, double bias) {
-    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+// CalcFeature + Normalize as 32 floats (miner descriptors).
+template <class P>
+__device__ __forceinline__ void descriptor(const TabView &T, int half_off, const P &pj, float (&f)[32]) {
+    f2 fp[16];
+    descriptor2(T, half_off, pj, fp);
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+        f[2 * j] = fp[j].x;
+        f[2 * j + 1] = fp[j].y;
+    }
+}
+
+// LogisticRegression::Predict (LogisticRegression.cpp:46-68); w4 = w[0..35]:
+// lane sums s0..s3 (s_j += w[4i+j]*f[4i+j], i = 0..7) as the pairs (s0, s1),
+// (s2, s3); z = (s0+s1)+(s2+s3); then the f64 bias term and sigmoid.
+__device__ __forceinline__ float lr_predict2(const f2 (&fp)[16], const float4 *w4, double bias) {
+    f2 s01 = f2{0.0f, 0.0f}, s23 = f2{0.0f, 0.0f};
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         const float4 wv = w4[i];
-        s0 = wv.x * f[4 * i + 0] + s0;
-        s1 = wv.y * f[4 * i + 1] + s1;
-        s2 = wv.z * f[4 * i + 2] + s2;
-        s3 = wv.w * f[4 * i + 3] + s3;
+        s01 = f2{wv.x, wv.y} * fp[2 * i] + s01;
+        s23 = f2{wv.z, wv.w} * fp[2 * i + 1] + s23;
     }
-    const float z32 = (s0 + s1) + (s2 + s3);
+    const float z32 = (s01.x + s01.y) + (s23.x + s23.y);
     double prob = (double)z32;
     prob += (double)w4[8].x * bias;
 #if SC_ABL_EXTRA_EXP  // timing ablation: one more f64 exp per item, result unused
@@ -187,11 +179,12 @@ __device__ __forceinline__ float lr_predict(const float (&f)[32], const float4 *
 }
 
 // One (window, weak classifier) item.
-__device__ __forceinline__ float weak_eval(const TabView &T, int half_off, const ProjPatch &pj,
-                                           const float4 *w4, double bias) {
-    float f[32];
-    descriptor(T, half_off, pj, f);
-    return lr_predict(f, w4, bias);
+template <class P>
+__device__ __forceinline__ float weak_eval(const TabView &T, int half_off, const P &pj, const float4 *w4,
+                                           double bias) {
+    f2 fp[16];
+    descriptor2(T, half_off, pj, fp);
+    return lr_predict2(fp, w4, bias);
 }
 
 }  // namespace sc

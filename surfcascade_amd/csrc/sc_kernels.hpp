@@ -36,9 +36,15 @@ struct TableGeom {
     int cs;    // float4 per cell step: 1 (channel-split halves) or 2 (8 channels together)
     int hs;    // float4 from a cell's channels 0-3 to its channels 4-7: ph*Qp or 1
     long long frame4;  // float4 per frame table = (H+1)*rowp
+    unsigned phm;      // ceil(2^32 / ph): x / ph = umulhi(x, phm) for the columns of a frame (host check)
     // float4 index of (x, half) within a table row
     __host__ __device__ int at(int x, int h) const {
         return cs * ((x % ph) * Qp + x / ph) + h * hs;
+    }
+    // at(x, 0) with the division by ph as a multiply-high (kernels)
+    __device__ __forceinline__ int at0(unsigned x) const {
+        const unsigned q = __umulhi(x, phm);
+        return cs * ((int)(x - q * (unsigned)ph) * Qp + (int)q);
     }
     // origin cell of grid window j (x = step*j) within its table row: windows
     // of one parity sit in consecutive cells when ph = 2*step
@@ -55,7 +61,8 @@ struct LevelInfo {
     float thr;            // (float)(l*lh) * prefilter_k   (ObjDetector.cpp:188)
     int pre_col[2];       // cell of column x+l relative to x, by window parity
     int pre_row;          // lh*rowp
-    int pad[2];
+    float scale;          // (float)l / tmpl_w   (DenseSURFFeatureExtractor.cpp:463)
+    int pad;
 };
 
 // A fitted patch projected to one level (ProjectPatches + GetRectsFromPatch,
@@ -66,6 +73,27 @@ struct ProjPatch {
     int row0;     // dy*rowp
     int rowstep;  // c*rowp
     int col[5];   // ((dx+i*c)%step)*Qp + (dx+i*c)/step, i = 0..gw
+    __device__ __forceinline__ int colq(int q) const { return col[q]; }
+};
+
+// A fitted patch as the template rect it was projected from: the chain
+// kernel projects it per item (ProjectPatches :459-484 + GetRectsFromPatch
+// :360-377, the same f32 multiplies and truncations as the host table) from
+// a 16-B record in LDS instead of fetching a ProjPatch from HBM: one
+// dependent global round trip less per item.
+//   x = px, y = py, z = the template side ProjectPatches scales (ph for
+//   square / wide, pw for tall), w = shape (0 2x2, 1 1x4 tall, 2 4x1 wide)
+struct InlinePatch {
+    int shape, row0, rowstep;
+    int x0;   // window column of the patch's left edge + the parity base column
+    int c;    // cell side
+    int cb;   // at0(parity base column)
+    unsigned phm;
+    int ph, Qp, cs;  // TableGeom (wave-uniform)
+    __device__ __forceinline__ int colq(int q) const {
+        const unsigned x = (unsigned)(x0 + q * c), qq = __umulhi(x, phm);
+        return cs * ((int)(x - qq * (unsigned)ph) * Qp + (int)qq) - cb;
+    }
 };
 
 constexpr int kStrip = 32;  // integral passes: pixels per strip (per 32-lane half wave)
@@ -104,6 +132,7 @@ struct CascadeArgs {
     TableGeom g;
     const TaskDesc *tasks;  // [n_bands][kXcds*n_sub]
     const ProjPatch *proj;  // [n_levels][2 parities][K]
+    const int4 *rects;      // [K]: template rect record of each weak (InlinePatch)
     const float4 *w;        // [K][9]: w[0..32] + 3 pad
     const double *bias;     // [K]
     const float *theta;     // [S]

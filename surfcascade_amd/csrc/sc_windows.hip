@@ -87,8 +87,13 @@ __host__ __device__ inline size_t wave_scratch_bytes(int SA) {
 // LW: weights and biases staged in LDS (else read through the caches: models
 // whose weights do not fit the LDS)
 __host__ __device__ inline size_t model_lds_bytes(int K, bool LW) {
-    return (LW ? (size_t)K * 144 + (size_t)K * 8 : 0) + (((size_t)K * 2 + 15) & ~(size_t)15);
+    return (LW ? (size_t)K * 144 + (size_t)K * 8 : 0) + (((size_t)K * 2 + 15) & ~(size_t)15) +
+           (size_t)K * 16;  // + template rect records (InlinePatch)
 }
+
+#ifndef SC_PROJ_INLINE  // chain kernel: project patches per item from LDS rects (0: ProjPatch table)
+#define SC_PROJ_INLINE 1
+#endif
 
 // A set of windows of one level: nr rows of nw windows; window (r, u) has
 // its origin cell (phase 0, half 0) at t_off + r*row_cells + u*wstep.
@@ -110,7 +115,7 @@ struct BandRows {  // full grid: nr rows of one level, windows j0 + u of row r
     __device__ float thr_of(int) const { return thr; }
     __device__ int pre_row_of(int) const { return pre_row; }
     __device__ int pre_col_of(int, int u) const { return ((j0 + u) & 1) ? pre_col1 : pre_col0; }
-    __device__ const ProjPatch *proj_of(int, int u) const { return projL + ((j0 + u) & 1) * K; }
+    __device__ ProjPatch patch(int, int u, int gk) const { return load_proj(projL + ((j0 + u) & 1) * K + gk); }
 };
 
 // chain kernel: one row per task slot, each with its own frame, level and
@@ -122,12 +127,17 @@ struct SlotDesc {
     int pre_row, pre_col;
     int proj;        // (level * 2 + parity) * K
     int r;           // the batch's first window, relative to the segment
+    float scale;     // the level's ProjectPatches scale
+    int xb;          // the parity's base column: step * parity
+    int cb;          // its table column: at(xb, 0)
     int pad;
 };
 struct SlotRows {
     const SlotDesc *d;
     int nr, bstride, wstep;
     const ProjPatch *proj;
+    const int4 *R;  // template rect records in LDS
+    TableGeom g;
     __device__ int rows() const { return nr; }
     __device__ int stride() const { return bstride; }
     __device__ int width(int r) const { return d[r].nw; }
@@ -135,7 +145,31 @@ struct SlotRows {
     __device__ float thr_of(int r) const { return d[r].thr; }
     __device__ int pre_row_of(int r) const { return d[r].pre_row; }
     __device__ int pre_col_of(int r, int) const { return d[r].pre_col; }
-    __device__ const ProjPatch *proj_of(int r, int) const { return proj + d[r].proj; }
+#if SC_PROJ_INLINE
+    // ProjectPatches (DenseSURFFeatureExtractor.cpp:459-484): x' = (int)(px*scale),
+    // y' likewise, the scaled side e = (int)(side*scale); GetRectsFromPatch
+    // (:360-377): square -> c = e/2 (2x2 cells), otherwise c = e (1x4 / 4x1).
+    // The host's ProjPatch table holds the same values (build_geometry).
+    __device__ InlinePatch patch(int r, int, int gk) const {
+        const int4 rc = R[gk];
+        const float s = d[r].scale;
+        const int px = (int)((float)rc.x * s), py = (int)((float)rc.y * s), e = (int)((float)rc.z * s);
+        InlinePatch p;
+        p.shape = rc.w;
+        p.c = rc.w == 0 ? (e >> 1) : e;
+        p.row0 = py * g.rowp;
+        p.rowstep = p.c * g.rowp;
+        p.x0 = d[r].xb + px;
+        p.cb = d[r].cb;
+        p.phm = g.phm;
+        p.ph = g.ph;
+        p.Qp = g.Qp;
+        p.cs = g.cs;
+        return p;
+    }
+#else
+    __device__ ProjPatch patch(int r, int, int gk) const { return load_proj(proj + d[r].proj + gk); }
+#endif
 };
 
 // The per-window work of the detect loop for the windows `need(slot)`
@@ -214,10 +248,10 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
                 if (i < nsurv) {
                     sv = surv[i];
                     const TabView Tj{Tb, cell(sv) << 4};
-                    const ProjPatch *projL = B.proj_of((int)(sv >> 16), (int)(sv & 0xffffu));
+                    const int sr = (int)(sv >> 16), su = (int)(sv & 0xffffu);
                     for (int k = 0; k < n; k++) {
                         const int gk = off + k;
-                        sum += weak_eval(Tj, half_off, projL[gk], a.w + gk * 9, a.bias[gk]);
+                        sum += weak_eval(Tj, half_off, B.patch(sr, su, gk), a.w + gk * 9, a.bias[gk]);
                     }
                 }
                 decide(i < nsurv, sv, sum);
@@ -245,7 +279,7 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
                     const int gk = off + k;
                     const unsigned sv = surv[c + i];
                     const TabView Tj{Tb, cell(sv) << 4};
-                    const ProjPatch pj = load_proj(B.proj_of((int)(sv >> 16), (int)(sv & 0xffffu)) + gk);
+                    const auto pj = B.patch((int)(sv >> 16), (int)(sv & 0xffffu), gk);
                     P[k * G + i] = LW ? weak_eval(Tj, half_off, pj, Wl + gk * 9, Bl[gk])
                                       : weak_eval(Tj, half_off, pj, a.w + gk * 9, a.bias[gk]);
                 }
@@ -267,16 +301,18 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
 // workgroup barrier: the waves are independent afterwards).
 template <bool LW>
 __device__ __forceinline__ void stage_model(const CascadeArgs &a, unsigned char *smem, float4 *&Wl,
-                                            double *&Bl, int16_t *&Ol) {
+                                            double *&Bl, int16_t *&Ol, int4 *&Rl) {
     const int K = a.K, tid = threadIdx.x;
     Wl = reinterpret_cast<float4 *>(smem);
     Bl = reinterpret_cast<double *>(smem + (LW ? (size_t)K * 144 : 0));
     Ol = reinterpret_cast<int16_t *>(Bl + (LW ? K : 0));
+    Rl = reinterpret_cast<int4 *>(reinterpret_cast<unsigned char *>(Ol) + (((size_t)K * 2 + 15) & ~(size_t)15));
     if (LW)
         for (int i = tid; i < K * 9; i += kCascadeThreads) Wl[i] = a.w[i];
     for (int i = tid; i < K; i += kCascadeThreads) {
         if (LW) Bl[i] = a.bias[i];
         Ol[i] = a.order[i];
+        Rl[i] = a.rects[i];
     }
     __syncthreads();
 }
@@ -294,7 +330,8 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
     float4 *Wl;
     double *Bl;
     int16_t *Ol;
-    stage_model<LW>(a, smem, Wl, Bl, Ol);
+    int4 *Rl;
+    stage_model<LW>(a, smem, Wl, Bl, Ol, Rl);
 
     const int SA = (a.strip_max * a.band_rows + 63) & ~63;
     unsigned char *ws = smem + model_lds_bytes(a.K, LW) + (size_t)wv * wave_scratch_bytes(SA);
@@ -525,11 +562,12 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
     float4 *Wl;
     double *Bl;
     int16_t *Ol;
+    int4 *Rl;
     // the level table in LDS: slot descriptors and merges read it every round
     LevelInfo *Lv = reinterpret_cast<LevelInfo *>(smem + model_lds_bytes(a.K, LW) +
                                                   kWavesPerWg * chain_wave_bytes(w.row_max));
     for (int i = threadIdx.x; i < w.n_levels; i += kCascadeThreads) Lv[i] = w.levels[i];
-    stage_model<LW>(a, smem, Wl, Bl, Ol);  // (its barrier covers Lv)
+    stage_model<LW>(a, smem, Wl, Bl, Ol, Rl);  // (its barrier covers Lv)
 
     const int sa = (w.row_max + 63) & ~63, nwords = sa >> 6;  // row_max: widest segment
     unsigned char *ws = smem + model_lds_bytes(a.K, LW) + (size_t)wv * chain_wave_bytes(w.row_max);
@@ -692,12 +730,15 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
                     dd.pre_col = (jb & 1) ? L.pre_col[1] : L.pre_col[0];  // (no dynamic index: scratch)
                     dd.proj = (level[sl] * 2 + (jb & 1)) * a.K;
                     dd.r = r[sl];
+                    dd.scale = L.scale;
+                    dd.xb = (jb & 1) * g.step;
+                    dd.cb = g.at0((unsigned)dd.xb);
                 }
                 desc[sl] = dd;
             }
         }
         wave_sync();
-        const SlotRows B{desc, kSlots, kBatch, g.ph == g.step ? 2 * cs : cs, a.proj};
+        const SlotRows B{desc, kSlots, kBatch, g.ph == g.step ? 2 * cs : cs, a.proj, Rl, g};
         auto need = [&](int slot) {  // window not evaluated yet (an earlier batch may have)
             const int sl = slot / kBatch, u = slot - sl * kBatch;
             const int k = desc[sl].r + 2 * u;
