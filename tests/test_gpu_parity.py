@@ -109,6 +109,18 @@ def test_grid_parity_kernel_paths(sc, oracle, face_cascade, monkeypatch, chunk_m
         assert T.view(np.uint32).tobytes() == oracle.integral(img).view(np.uint32).tobytes()
 
 
+@pytest.mark.parametrize("order,block", [("0", None), ("1", None), ("2", "5")])
+def test_chain_row_orders(sc, oracle, face_cascade, monkeypatch, order, block):
+    """The chain kernel's task order (level-major, y-major, other row blocks
+    than the default 64) changes the schedule only, never the bits."""
+    monkeypatch.setenv("SC_ROW_ORDER", order)
+    if block:
+        monkeypatch.setenv("SC_ROW_BLOCK", block)
+    img = _frame(1280, 720, 78)
+    _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=8),
+                 oracle.Params(n_levels=8))
+
+
 @pytest.mark.parametrize("lds_weights", [None, "0"])
 def test_pedestrian_64x128(sc, oracle, ped_cascade, monkeypatch, lds_weights):
     if lds_weights:  # the cache-read weights variant (models too big for the LDS)
