@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--model")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--host-steps", type=int, default=5,
+                    help="steps of the host-buffer boundary leg (PCIe-inclusive rate; 0: skip)")
     a = ap.parse_args()
     c = CONFIGS[a.config]
     if a.batch is None and a.shard == "grid":
@@ -179,6 +181,15 @@ def main():
     det.set_timing(False)
     kt = det.get_timing()
     visited = det.info("visited")
+    # the host-buffer boundary (sc_detect_batch: pageable u8 frames in, raw
+    # windows out, H2D + D2H over PCIe inside): reported beside, never `value`
+    host_dt = None
+    if args.host_steps > 0 and not grid_shard:
+        det.detect_batch(host_frames)
+        t1 = time.perf_counter()
+        for _ in range(args.host_steps):
+            det.detect_batch(host_frames)
+        host_dt = (time.perf_counter() - t1) / args.host_steps
     if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64, device=frames.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -243,6 +254,11 @@ def main():
             "visited_windows_last_step": visited,
             "detections_last_step": total_det,
         }
+        if host_dt is not None:
+            line["pcie_inclusive"] = {
+                "value": grid * B / host_dt, "unit": "windows/s", "ms_per_step": host_dt * 1e3,
+                "steps": args.host_steps, "per": "GPU",
+                "path": "sc_detect_batch: %d pageable host frames in (H2D), raw windows out (D2H)" % B}
         if not args.no_cpu and world == 1:
             line["cpu_baseline"] = cpu_baseline(host_frames, args.model, args.levels, args.cpu_seconds,
                                                 args.pedestrian)

@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 #include <cfloat>
 #include <cstdint>
@@ -182,11 +183,37 @@ struct SlotRows {
 //      lanes in shape-sorted weak order, results through LDS, each survivor's
 //      lane adds them in the model's k order (GentleAdaboost.cpp:255-258);
 //      the theta test (:197) and order-preserving compaction.
-template <bool LW, class Rows, class Need>
+// Item-schedule counters of profiling builds (SC_PROF_CHAIN): wave-uniform.
+struct NoStats {
+    [[maybe_unused]] static constexpr bool on = false;
+    __device__ void iter(int) {}
+    __device__ void stage(int) {}
+    __device__ void pre(int, int) {}
+};
+struct ItemStats {
+    [[maybe_unused]] static constexpr bool on = true;
+    unsigned long long iters = 0, lanes = 0, thin16 = 0, thin32 = 0, stages = 0, surv = 0, need = 0, pass = 0;
+    __device__ void iter(int active) {  // one item iteration (a gather round trip)
+        iters++;
+        lanes += (unsigned)active;
+        thin16 += active <= 16;
+        thin32 += active <= 32;
+    }
+    __device__ void stage(int nsurv) {
+        stages++;
+        surv += (unsigned)nsurv;
+    }
+    __device__ void pre(int n_need, int n_pass) {
+        need += (unsigned)n_need;
+        pass += (unsigned)n_pass;
+    }
+};
+
+template <bool LW, class Rows, class Need, class Stats = NoStats>
 __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B, const char *Tb,
                                              const float4 *Wl, const double *Bl, const int16_t *Ol,
                                              float *P, float *st_s, unsigned *surv, int8_t *st_p,
-                                             int lane, Need need) {
+                                             int lane, Need need, Stats &&stats = Stats{}) {
     const int half_off = a.g.hs, stride = B.stride();
     const float4 *T = reinterpret_cast<const float4 *>(Tb);
     auto cell = [&](unsigned sv) { return B.origin((int)(sv >> 16), (int)(sv & 0xffffu)); };
@@ -212,6 +239,8 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
             const unsigned long long mk = __ballot(pass);
             if (pass) surv[nsurv + __popcll(mk & lanes_below())] = ((unsigned)r << 16) | (unsigned)u;
             nsurv += __popcll(mk);
+            if constexpr (std::remove_reference_t<Stats>::on)
+                stats.pre(__popcll(__ballot(u < nw && need(r * stride + u))), __popcll(mk));
         }
     }
     wave_sync();
@@ -221,6 +250,7 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
         const int off = a.stage_off[s], n = a.stage_off[s + 1] - off;
         const float th = a.theta[s];
         int nn = 0;
+        stats.stage(nsurv);
         // stage decision of one survivor (GentleAdaboost.cpp:259;
         // ObjDetector.cpp:197) and in-place order-preserving compaction:
         // kept survivors move to [nn, ...), never past the group just read
@@ -242,6 +272,7 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
         if (nsurv >= a.chunk_min || n > kItemBuf) {
             // one lane per survivor, k wave-uniform: parameters via scalar loads
             for (int c = 0; c < nsurv; c += 64) {
+                stats.iter(min(64, nsurv - c));
                 const int i = c + lane;
                 unsigned sv = 0;
                 float sum = 0.0f;
@@ -273,6 +304,7 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
                     else if (i >= G) { kk++; i -= G; }
                     k = Ol[off + kk];
                 };
+                for (int b2 = 0; b2 < items; b2 += 64) stats.iter(min(64, items - b2));
                 for (int t2 = lane; t2 < items; t2 += 64) {
                     int k, i;
                     decode(t2, k, i);
@@ -600,6 +632,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
 #if SC_PROF_CHAIN
     unsigned long long c_idle = 0, c_setup = 0, c_eval = 0, c_merge = 0, n_rounds = 0, n_slots = 0;
     unsigned long long c_deq = 0, c_poll = 0;
+    ItemStats istats;
     unsigned long long t_last = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -760,8 +793,13 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
         }
         wave_sync();
         SC_PROF(c_setup);
+#if SC_PROF_CHAIN
+        eval_windows<LW>(a, B, reinterpret_cast<const char *>(a.table), Wl, Bl, Ol, P, st_s, surv,
+                         st_p, lane, need, istats);
+#else
         eval_windows<LW>(a, B, reinterpret_cast<const char *>(a.table), Wl, Bl, Ol, P, st_s, surv,
                          st_p, lane, need);
+#endif
         wave_sync();
         SC_PROF(c_eval);
 #if SC_PROF_CHAIN
@@ -873,6 +911,14 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
         atomicAdd(&w.prof[5], n_slots);
         atomicAdd(&w.prof[6], c_deq);
         atomicAdd(&w.prof[7], c_poll);
+        atomicAdd(&w.prof[8], istats.iters);
+        atomicAdd(&w.prof[9], istats.lanes);
+        atomicAdd(&w.prof[10], istats.thin16);
+        atomicAdd(&w.prof[11], istats.thin32);
+        atomicAdd(&w.prof[12], istats.stages);
+        atomicAdd(&w.prof[13], istats.surv);
+        atomicAdd(&w.prof[14], istats.need);
+        atomicAdd(&w.prof[15], istats.pass);
     }
 #endif
 }
