@@ -399,12 +399,18 @@ class Detector:
         return out[:n.value]
 
     def detect_batch(self, frames, capacity=1 << 18):
-        frames = np.ascontiguousarray(frames, np.uint8)
+        # frames go in as they lie when their rows are unit-stride (per-frame
+        # pointers + row stride, as sc_detect_batch takes them); other layouts
+        # are made row-major first
+        frames = np.asarray(frames)
+        if frames.dtype != np.uint8 or frames.ndim != 3 or frames.strides[2] != 1 \
+                or frames.strides[1] < frames.shape[2]:
+            frames = np.ascontiguousarray(frames, np.uint8)
         nf, H, W = frames.shape
         ptrs = (ctypes.c_void_p * nf)(*[frames[i].ctypes.data for i in range(nf)])
         out = np.zeros(capacity, WINDOW_DTYPE)
         counts = (ctypes.c_int * nf)()
-        _check(load_library().sc_detect_batch(self._h, ptrs, nf, W, H, W, out.ctypes.data,
+        _check(load_library().sc_detect_batch(self._h, ptrs, nf, W, H, frames.strides[1], out.ctypes.data,
                                               capacity, counts))
         res, o = [], 0
         for c in counts:
@@ -413,11 +419,24 @@ class Detector:
         return res
 
     # -- device frames (torch uint8 tensor [n, H, W] on this device) --------
-    def detect_device(self, frames, capacity=1 << 18):
+    @staticmethod
+    def _device_frames(frames):
+        """(n, H, W, row stride) of a uint8 [n, H, W] device tensor whose
+        frames sit at data_ptr + f*H*stride with unit-stride rows (the C ABI's
+        layout, sc_detect_device); anything else is refused, not copied."""
+        if frames.dim() != 3 or frames.element_size() != 1 or not frames.is_cuda:
+            raise ValueError("frames must be a uint8 [n, H, W] device tensor")
         n, H, W = frames.shape
+        s0, s1, s2 = frames.stride()
+        if s2 != 1 or s1 < W or (n > 1 and s0 != H * s1):
+            raise ValueError("frames must be row-major [n, H, W] (strides %s)" % (frames.stride(),))
+        return n, H, W, s1
+
+    def detect_device(self, frames, capacity=1 << 18):
+        n, H, W, rs = self._device_frames(frames)
         out = np.zeros(capacity, WINDOW_DTYPE)
         counts = (ctypes.c_int * n)()
-        _check(load_library().sc_detect_device(self._h, frames.data_ptr(), n, W, H, W,
+        _check(load_library().sc_detect_device(self._h, frames.data_ptr(), n, W, H, rs,
                                                out.ctypes.data, capacity, counts))
         res, o = [], 0
         for c in counts:
@@ -427,9 +446,9 @@ class Detector:
 
     def enqueue_device(self, frames, out_records, counts):
         """Async: out_records = torch uint8 [cap*40] (RECORD_DTYPE), counts = int32 [1+n]."""
-        n, H, W = frames.shape
+        n, H, W, rs = self._device_frames(frames)
         cap = out_records.numel() * out_records.element_size() // RECORD_DTYPE.itemsize
-        _check(load_library().sc_enqueue_device(self._h, frames.data_ptr(), n, W, H, W,
+        _check(load_library().sc_enqueue_device(self._h, frames.data_ptr(), n, W, H, rs,
                                                 out_records.data_ptr(), cap, counts.data_ptr()))
 
     def synchronize(self):

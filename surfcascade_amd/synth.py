@@ -55,7 +55,9 @@ def make_frame(W: int, H: int, seed: int) -> np.ndarray:
         else:
             patch[mask] = val
     img += rng.normal(0, 3.0, size=img.shape).astype(np.float32)
-    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+    # row-major like every frame the C ABI takes (the bilinear broadcast above
+    # leaves img column-major; a column-major batch costs a full copy per call)
+    return np.ascontiguousarray(np.clip(np.rint(img), 0, 255).astype(np.uint8))
 
 
 def make_frames(W: int, H: int, n: int, seed0: int = 1000) -> np.ndarray:

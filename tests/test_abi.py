@@ -83,3 +83,14 @@ def test_no_gpu_is_a_device_error_not_a_crash(sc):
     with pytest.raises(sc.SurfCascadeError) as e:
         sc.Detector(c)
     assert e.value.code == -5
+
+
+def test_frame_layouts(sc):
+    # synthetic frames are row-major (a column-major batch costs the host
+    # boundary a full copy per call); device wrappers refuse what the C ABI
+    # would misread
+    import torch
+    from surfcascade_amd import synth
+    assert synth.make_frames(64, 48, 2).flags["C_CONTIGUOUS"]
+    with pytest.raises(ValueError):
+        sc.Detector._device_frames(torch.zeros(2, 48, 64, dtype=torch.uint8))  # host tensor

@@ -212,6 +212,24 @@ def test_device_resident_frames(sc, oracle, face_cascade):
         assert _det_set(res[k]) == _det_set(ref)
 
 
+def test_strided_frames(sc, oracle, face_cascade):
+    # frames handed over as row-strided views (a crop of wider buffers): host
+    # batch through per-frame pointers + row stride, device tensor likewise
+    import torch
+    wide = np.stack([_frame(700, 480, 310 + k) for k in range(2)])
+    view = wide[:, :, 30:670]
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=4))
+    host = det.detect_batch(view)
+    dev = det.detect_device(torch.from_numpy(wide).to("cuda:0")[:, :, 30:670])
+    for k in range(2):
+        T = oracle.integral(np.ascontiguousarray(view[k]))
+        ref, _ = oracle.detect(T, face_cascade, oracle.Params(n_levels=4))
+        assert _det_set(host[k]) == _det_set(ref)
+        assert _det_set(dev[k]) == _det_set(ref)
+    with pytest.raises(ValueError):  # column-major frames are refused, not misread
+        det.detect_device(torch.from_numpy(wide).to("cuda:0").transpose(1, 2))
+
+
 def test_capacity_error_reports_count(sc):
     from surfcascade_amd import synth
     from oracle import oracle as O
