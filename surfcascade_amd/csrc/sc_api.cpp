@@ -383,15 +383,16 @@ void build_geometry(sc_detector *d, int W, int H) {
         ng.n_bands = (int)(ng.tasks.size() / nseg);
     }
     {   // the chain kernel's task order (its queues deal rows in this order):
-        // 2 (default): blocks of 64 grid rows (192 px at step 3), level-major
+        // 2 (default): blocks of 32 grid rows (96 px at step 3), level-major
         // inside -- the rows in flight on an XCD then read a band of table
-        // rows that fits its L2: L2 misses halved and 8.5 % less kernel time
-        // against plain level-major order (0) on the C2 frames; 1: y-major.
+        // rows that fits its L2: 14 % less kernel time than plain level-major
+        // order (0) on the C2 frames; blocks of 64 rows 1 % and of 128 rows
+        // 3 % slower than 32 (profiles/r1/sweep); 1: y-major.
         // (The full-grid tasks above are built from the level-major list.)
         const char *e = std::getenv("SC_ROW_ORDER");  // tuning overrides
         const int mode = e ? std::atoi(e) : 2;
         const char *eb = std::getenv("SC_ROW_BLOCK");
-        const int blk = std::max(1, eb ? std::atoi(eb) : 64) * ng.step;
+        const int blk = std::max(1, eb ? std::atoi(eb) : 32) * ng.step;
         if (mode == 1)
             std::stable_sort(ng.rows.begin(), ng.rows.end(),
                              [](const int2 &a, const int2 &b) { return a.y < b.y; });

@@ -73,6 +73,13 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// A wave-uniform 64-bit value (read by every lane) into SGPRs.
+__device__ __forceinline__ unsigned long long uniform64(unsigned long long v) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 __device__ __forceinline__ unsigned xcc_id() {
     unsigned x;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
@@ -707,17 +714,25 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
                 }
                 SC_PROF(c_deq);
             }
-            if (st[sl] == 1) {  // poll once; a lost hand-off must not hang the GPU
-                int e = 0;
-                if (lane == 0)
-                    e = __hip_atomic_load(&w.entry[(long long)tt[sl] * kXcds + tq[sl]], __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-                e = __builtin_amdgcn_readfirstlane(e);
-                if (e) start(sl, e - 1);
-                SC_PROF(c_poll);
+        }
+        {   // poll every waiting slot once, the loads in flight together; a lost
+            // hand-off must not hang the GPU (watchdog below)
+            int e[kSlots];
+#pragma unroll
+            for (int sl = 0; sl < kSlots; sl++) {
+                e[sl] = 0;
+                if (st[sl] == 1 && lane == 0)
+                    e[sl] = __hip_atomic_load(&w.entry[(long long)tt[sl] * kXcds + tq[sl]], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
             }
-            n_active += st[sl] == 2;
-            n_wait += st[sl] == 1;
+#pragma unroll
+            for (int sl = 0; sl < kSlots; sl++) {
+                const int es = __builtin_amdgcn_readfirstlane(e[sl]);
+                if (st[sl] == 1 && es) start(sl, es - 1);
+                n_active += st[sl] == 2;
+                n_wait += st[sl] == 1;
+            }
+            SC_PROF(c_poll);
         }
         if (n_active == 0) {
             SC_PROF(c_idle);
@@ -851,14 +866,23 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
             wave_sync();
             int rr = r[sl];
             const int ns = nseg[sl];
+            // the segment's bit words, read once per word into SGPRs (the
+            // chain lands on a good window many times per word)
+            int cw = -1;
+            unsigned long long evw = 0, gdw = 0, dtw = 0;
             for (;;) {  // from a landing position: every second window until a good one
                 const int c = rr >> 6, b = rr & 63;
+                if (c != cw) {
+                    evw = uniform64(ev_[c]);
+                    gdw = uniform64(gd_[c]);
+                    dtw = uniform64(dt_[c]);
+                    cw = c;
+                }
                 const unsigned long long par = (b & 1) ? ~kEven : kEven;
                 const int lim = min(64, ns - (c << 6));  // bits past the segment
                 const unsigned long long inseg = lim == 64 ? ~0ull : ((1ull << lim) - 1ull);
                 const unsigned long long path = par & (~0ull << b) & inseg;
-                const unsigned long long evw = ev_[c];
-                const unsigned long long unev = path & ~evw, good = path & evw & gd_[c];
+                const unsigned long long unev = path & ~evw, good = path & evw & gdw;
                 const int f = unev ? __builtin_ctzll(unev) : 64;
                 const int qg = good ? __builtin_ctzll(good) : 64;
                 unsigned long long vis;
@@ -868,7 +892,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
                 } else if (qg < 64) {  // lands on good window qg, continues at qg + 1
                     vis = path & (qg == 63 ? ~0ull : ((2ull << qg) - 1ull));
                     const int k = (c << 6) + qg;
-                    if (lane == 0 && ((dt_[c] >> qg) & 1ull)) {  // detection (:203)
+                    if (lane == 0 && ((dtw >> qg) & 1ull)) {  // detection (:203)
                         const int slot = atomicAdd(&w.counters[0], 1);
                         atomicAdd(&w.counters[1 + w.frame0 + fr], 1);
                         if (slot < w.capacity) {
