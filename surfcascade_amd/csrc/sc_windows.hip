@@ -44,8 +44,11 @@ namespace {
 #define SC_CASCADE_MIN_WGS 1
 #endif
 
-#ifndef SC_CHAIN_MIN_WGS  // chain kernel: 3 workgroups (12 waves) per CU
-#define SC_CHAIN_MIN_WGS 3
+#ifndef SC_CHAIN_WAVES  // chain kernel: waves per workgroup (the model is staged once per workgroup:
+#define SC_CHAIN_WAVES 12  // one 12-wave workgroup per CU leaves the LDS room for 128-window batches)
+#endif
+#ifndef SC_CHAIN_MIN_WGS  // chain kernel: 12 waves per CU
+#define SC_CHAIN_MIN_WGS (12 / SC_CHAIN_WAVES)
 #endif
 
 #ifndef SC_ABL_NOWAIT  // timing ablation only: segments start without the hand-off (wrong results)
@@ -60,6 +63,8 @@ constexpr int kWavesPerWg = 4;
 constexpr int kItemBuf = SC_ITEM_BUF;
 constexpr int kWalkMaxChunks = 64;  // windows per row <= 4096 (host check)
 constexpr int kCascadeThreads = 64 * kWavesPerWg;
+constexpr int kChainWaves = SC_CHAIN_WAVES;
+constexpr int kChainThreads = 64 * kChainWaves;
 
 __device__ __forceinline__ unsigned long long lanes_below() {
     return (1ull << (threadIdx.x & 63)) - 1ull;
@@ -338,7 +343,7 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
 
 // The model staged in LDS once per persistent workgroup (the only
 // workgroup barrier: the waves are independent afterwards).
-template <bool LW>
+template <bool LW, int NT = kCascadeThreads>
 __device__ __forceinline__ void stage_model(const CascadeArgs &a, unsigned char *smem, float4 *&Wl,
                                             double *&Bl, int16_t *&Ol, int4 *&Rl) {
     const int K = a.K, tid = threadIdx.x;
@@ -347,8 +352,8 @@ __device__ __forceinline__ void stage_model(const CascadeArgs &a, unsigned char 
     Ol = reinterpret_cast<int16_t *>(Bl + (LW ? K : 0));
     Rl = reinterpret_cast<int4 *>(reinterpret_cast<unsigned char *>(Ol) + (((size_t)K * 2 + 15) & ~(size_t)15));
     if (LW)
-        for (int i = tid; i < K * 9; i += kCascadeThreads) Wl[i] = a.w[i];
-    for (int i = tid; i < K; i += kCascadeThreads) {
+        for (int i = tid; i < K * 9; i += NT) Wl[i] = a.w[i];
+    for (int i = tid; i < K; i += NT) {
         if (LW) Bl[i] = a.bias[i];
         Ol[i] = a.order[i];
         Rl[i] = a.rects[i];
@@ -558,9 +563,10 @@ static_assert(kSubQ >= 1 && kSubQ <= kMaxSubQ, "sub-queue count");
 #endif
 constexpr int kSlots = SC_CHAIN_SLOTS;
 #ifndef SC_CHAIN_BATCH
-#define SC_CHAIN_BATCH 64
+#define SC_CHAIN_BATCH 128
 #endif
 constexpr int kBatch = SC_CHAIN_BATCH;  // chain kernel: windows of one parity per slot and round
+constexpr int kBatchChunks = (kBatch + 63) / 64;
 static_assert(kBatch % 4 == 0 && kItemBuf % 4 == 0, "chain LDS carve: keep the u64 bit arrays aligned");
 
 // chain kernel LDS per wave: P f32[kItemBuf] | st_s f32[kSlots*kBatch] |
@@ -590,11 +596,13 @@ __host__ __device__ inline size_t chain_wave_bytes(int seg_max) {
 // and publishes where the chain leaves the segment.  A wave carries kSlots
 // tasks at once and evaluates their batches together (one prefilter pass,
 // one set of stage rounds), so the stage-by-stage round trips serve twice
-// the windows.  On the C2 frames the lazy grid evaluates ~55 % of the grid's
-// weak items (the visited windows alone are 53 %).  Visited windows that
+// the windows.  One workgroup of kChainWaves independent waves per CU (the
+// model staged in LDS once per CU).  On the C2 frames the lazy grid
+// evaluates ~55 % of the grid's weak items (the visited windows alone are
+// 53 %).  Visited windows that
 // passed every stage are emitted with score (s + S + 1)/S (:201-212).
 template <bool LW>
-__global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kernel(CascadeArgs a,
+__global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(CascadeArgs a,
                                                                                   WalkArgs w) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -604,9 +612,9 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
     int4 *Rl;
     // the level table in LDS: slot descriptors and merges read it every round
     LevelInfo *Lv = reinterpret_cast<LevelInfo *>(smem + model_lds_bytes(a.K, LW) +
-                                                  kWavesPerWg * chain_wave_bytes(w.row_max));
-    for (int i = threadIdx.x; i < w.n_levels; i += kCascadeThreads) Lv[i] = w.levels[i];
-    stage_model<LW>(a, smem, Wl, Bl, Ol, Rl);  // (its barrier covers Lv)
+                                                  kChainWaves * chain_wave_bytes(w.row_max));
+    for (int i = threadIdx.x; i < w.n_levels; i += kChainThreads) Lv[i] = w.levels[i];
+    stage_model<LW, kChainThreads>(a, smem, Wl, Bl, Ol, Rl);  // (its barrier covers Lv)
 
     const int sa = (w.row_max + 63) & ~63, nwords = sa >> 6;  // row_max: widest segment
     unsigned char *ws = smem + model_lds_bytes(a.K, LW) + (size_t)wv * chain_wave_bytes(w.row_max);
@@ -633,7 +641,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
     // serialise on its line).  A drained sub-queue sends the wave on to the
     // next one, then to the other XCDs' queues.
     int q = (int)xcc_id(), empty = 0;
-    int u = (int)((blockIdx.x / kXcds * kWavesPerWg + wv) % kSubQ);
+    int u = (int)((blockIdx.x / kXcds * kChainWaves + wv) % kSubQ);
     bool drained = false;
     unsigned idle = 0;  // rounds with every task waiting for its entry
 #if SC_PROF_CHAIN
@@ -792,9 +800,15 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
             const int k = desc[sl].r + 2 * u;
             return ((evb(sl)[k >> 6] >> (k & 63)) & 1ull) == 0ull;
         };
-        bool mine[kSlots];
+        // the windows this round evaluates, window c*64 + lane of each slot's batch
+        unsigned long long mine[kSlots][kBatchChunks];
 #pragma unroll
-        for (int sl = 0; sl < kSlots; sl++) mine[sl] = st[sl] == 2 && lane < desc[sl].nw && need(sl * kBatch + lane);
+        for (int sl = 0; sl < kSlots; sl++)
+#pragma unroll
+            for (int c = 0; c < kBatchChunks; c++) {
+                const int u = c * 64 + lane;
+                mine[sl][c] = __ballot(st[sl] == 2 && u < desc[sl].nw && need(sl * kBatch + u));
+            }
         // park the slot state in LDS across the evaluation: it would otherwise
         // stay live in SGPRs / VGPR lanes through the register-heavy item loop
         if (lane == 0) {
@@ -846,9 +860,12 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CHAIN_MIN_WGS) void chain_kerne
                                   (long long)(y / w.step) * L.nx + j0[sl];
             unsigned long long *ev_ = evb(sl), *gd_ = gdb(sl), *dt_ = dtb(sl);
             float *sg = s_seg(sl);
-            if (mine[sl]) {
-                const int k = r[sl] + 2 * lane, p = st_p[sl * kBatch + lane];
-                const float sc = st_s[sl * kBatch + lane];
+#pragma unroll
+            for (int c = 0; c < kBatchChunks; c++) {
+                if (!((mine[sl][c] >> lane) & 1ull)) continue;
+                const int u = c * 64 + lane;
+                const int k = r[sl] + 2 * u, p = st_p[sl * kBatch + u];
+                const float sc = st_s[sl * kBatch + u];
                 bool good = false;
                 if (p >= 0) {
                     const double fin = ((double)sc + p + 1) / S;  // ObjDetector.cpp:201
@@ -983,7 +1000,7 @@ void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s) {
 }
 
 int launch_chain(const CascadeArgs &a, const WalkArgs &w, int device, hipStream_t s) {
-    const size_t scratch = kWavesPerWg * chain_wave_bytes(w.row_max) + w.n_levels * sizeof(LevelInfo);
+    const size_t scratch = kChainWaves * chain_wave_bytes(w.row_max) + w.n_levels * sizeof(LevelInfo);
     bool lw = model_lds_bytes(a.K, true) + scratch <= 160 * 1024;
     if (const char *e = std::getenv("SC_LDS_WEIGHTS")) lw = std::atoi(e) != 0;  // tuning override
     const size_t lds = model_lds_bytes(a.K, lw) + scratch;
@@ -994,22 +1011,22 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, int device, hipStream_
     }
     int per_cu = 0;
     if (lw)
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<true>, kCascadeThreads, lds);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<true>, kChainThreads, lds);
     else
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<false>, kCascadeThreads, lds);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<false>, kChainThreads, lds);
     per_cu = std::max(1, std::min(per_cu, 4));
     if (const char *e = std::getenv("SC_WGS_PER_CU"))  // tuning override
         per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
     const int grid = std::max(1, cus) * per_cu;
     if (lw)
-        hipLaunchKernelGGL(chain_kernel<true>, dim3(grid), dim3(kCascadeThreads), lds, s, a, w);
+        hipLaunchKernelGGL(chain_kernel<true>, dim3(grid), dim3(kChainThreads), lds, s, a, w);
     else
-        hipLaunchKernelGGL(chain_kernel<false>, dim3(grid), dim3(kCascadeThreads), lds, s, a, w);
+        hipLaunchKernelGGL(chain_kernel<false>, dim3(grid), dim3(kChainThreads), lds, s, a, w);
     return grid;
 }
 
 size_t chain_lds_bytes(int K, int row_max, int n_levels) {  // smallest variant
-    return model_lds_bytes(K, false) + kWavesPerWg * chain_wave_bytes(row_max) +
+    return model_lds_bytes(K, false) + kChainWaves * chain_wave_bytes(row_max) +
            n_levels * sizeof(LevelInfo);
 }
 
