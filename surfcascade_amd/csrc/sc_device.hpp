@@ -113,6 +113,87 @@ __device__ __forceinline__ void patch_features2(const TabView &T, const P &pj, i
             }
 }
 
+// The same CalcFeature split in two phases for the software-pipelined item
+// loop: corner loads into a fixed 20-entry array (2 halves x up to 10
+// corners, index h*10 + r*(GW+1) + c), then the box sums from it.
+template <int GW, int GH, class P>
+__device__ __forceinline__ void patch_load(const TabView &T, const P &pj, int half_off, float4 (&cn)[20]) {
+    int col[GW + 1];
+#pragma unroll
+    for (int c = 0; c <= GW; c++) col[c] = pj.colq(c);
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int r = 0; r <= GH; r++) {
+            const int ro = h * half_off + pj.row0 + r * pj.rowstep;
+#pragma unroll
+            for (int c = 0; c <= GW; c++) cn[h * 10 + r * (GW + 1) + c] = T.at(ro + col[c]);
+        }
+}
+
+template <int GW, int GH>
+__device__ __forceinline__ void patch_box(const float4 (&cn)[20], f2 (&fp)[16]) {
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int r = 0; r < GH; r++)
+#pragma unroll
+            for (int c = 0; c < GW; c++) {
+                // (TL + BR) - (TR + BL), :385-412
+                const float4 tl = cn[h * 10 + r * (GW + 1) + c];
+                const float4 br = cn[h * 10 + (r + 1) * (GW + 1) + c + 1];
+                const float4 tr = cn[h * 10 + r * (GW + 1) + c + 1];
+                const float4 bl = cn[h * 10 + (r + 1) * (GW + 1) + c];
+                const int o = 4 * (r * GW + c) + 2 * h;
+                fp[o] = (f2{tl.x, tl.y} + f2{br.x, br.y}) - (f2{tr.x, tr.y} + f2{bl.x, bl.y});
+                fp[o + 1] = (f2{tl.z, tl.w} + f2{br.z, br.w}) - (f2{tr.z, tr.w} + f2{bl.z, bl.w});
+            }
+}
+
+#ifndef SC_ULOAD  // corners_load: one straight-line set of 20 loads for every shape
+#define SC_ULOAD 0
+#endif
+template <class P>
+__device__ __forceinline__ void corners_load(const TabView &T, int half_off, const P &pj, float4 (&cn)[20]) {
+#if SC_ULOAD
+    // slot m of a half holds corner (r, c): 2x2 m = 3r + c (slot 9 repeats
+    // (2, 2)), 1x4 m = 2r + c, 4x1 m = 5r + c; the shapes differ only in the
+    // per-lane offsets, so the loads issue without divergence
+    int col[5], ro[5];
+#pragma unroll
+    for (int c = 0; c < 5; c++) col[c] = pj.colq(c);
+#pragma unroll
+    for (int r = 0; r < 5; r++) ro[r] = pj.row0 + r * pj.rowstep;
+    const bool sq = pj.shape == 0, tall = pj.shape == 1;
+    int off[10];
+#pragma unroll
+    for (int m = 0; m < 10; m++) {
+        const int o0 = ro[m < 9 ? m / 3 : 2] + col[m < 9 ? m % 3 : 2];
+        const int o1 = ro[m / 2] + col[m % 2];
+        const int o2 = ro[m / 5] + col[m % 5];
+        off[m] = sq ? o0 : (tall ? o1 : o2);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int m = 0; m < 9; m++) cn[h * 10 + m] = T.at(h * half_off + off[m]);
+    if (!sq) {  // the strips' tenth corners (a 2x2 patch has 9)
+        cn[9] = T.at(off[9]);
+        cn[19] = T.at(half_off + off[9]);
+    }
+#else
+    if (pj.shape == 0) patch_load<2, 2>(T, pj, half_off, cn);
+    else if (pj.shape == 1) patch_load<1, 4>(T, pj, half_off, cn);
+    else patch_load<4, 1>(T, pj, half_off, cn);
+#endif
+}
+
+__device__ __forceinline__ void corners_box(int shape, const float4 (&cn)[20], f2 (&fp)[16]) {
+    if (shape == 0) patch_box<2, 2>(cn, fp);
+    else if (shape == 1) patch_box<1, 4>(cn, fp);
+    else patch_box<4, 1>(cn, fp);
+}
+
 // c_k = (q0+q1)+(q2+q3) of f[4k..4k+3] = fp[2k], fp[2k+1];
 // SS = (((eps + c0) + c1) ...) + c7   (:427-433)
 __device__ __forceinline__ float ss_hadd2(const f2 (&fp)[16]) {
@@ -125,12 +206,19 @@ __device__ __forceinline__ float ss_hadd2(const f2 (&fp)[16]) {
     return ss;
 }
 
+// Normalize (:417-457) of the 32 box sums in place.
+__device__ __forceinline__ void normalize2(f2 (&fp)[16]);
+
 // CalcFeature + Normalize (:379-457) of one projected patch.
 template <class P>
 __device__ __forceinline__ void descriptor2(const TabView &T, int half_off, const P &pj, f2 (&fp)[16]) {
     if (pj.shape == 0) patch_features2<2, 2>(T, pj, half_off, fp);
     else if (pj.shape == 1) patch_features2<1, 4>(T, pj, half_off, fp);
     else patch_features2<4, 1>(T, pj, half_off, fp);
+    normalize2(fp);
+}
+
+__device__ __forceinline__ void normalize2(f2 (&fp)[16]) {
     const float theta = 0.35355338f;  // 2/sqrt(32.f) (.h:36)
     const float t = sqrtf(ss_hadd2(fp)) * theta, nt = -t;
     // _mm_max_ps(_mm_min_ps(f, t), -t) as one v_med3_f32: identical bits here
