@@ -146,6 +146,13 @@ int sc_miner_create(const sc_model *m, int tmpl_w, int tmpl_h, int device,
  * *n_out = all candidates; SC_ERR_CAPACITY when that exceeds capacity. */
 int sc_mine(sc_detector *d, const uint8_t *gray, int w, int h, int stride_bytes,
             sc_window *wins, float *features, int capacity, int *n_out);
+/* sc_mine on a frame already in device memory, the descriptors written
+ * straight into d_features (device memory, float[capacity][n_patches][32], or
+ * NULL): no host copy of the descriptors, which dominates sc_mine when many
+ * are kept (FillNegSamples' sample matrix, DenseSURFFeatureExtractor.cpp:
+ * 124-195, stays on the GPU for the trainer).  Windows still go to the host. */
+int sc_mine_device(sc_detector *d, const uint8_t *d_gray, int w, int h, int stride_bytes,
+                   sc_window *wins, float *d_features, int capacity, int *n_out);
 
 /* ---- introspection / parity dumps -------------------------------------- */
 #define SC_INFO_LEVELS 1        /* levels used for the last geometry         */

@@ -49,7 +49,7 @@ EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_mode
            "sc_enqueue_device", "sc_synchronize", "sc_detector_stream", "sc_detector_info",
            "sc_detector_set_shard", "sc_detector_set_debug", "sc_debug_dump", "sc_set_timing", "sc_get_timing",
            "sc_group_rectangles", "sc_group_detections", "sc_fddb_format",
-           "sc_miner_create", "sc_mine", "sc_fast_nms", "sc_decode_jpeg_gray", "sc_imread_gray",
+           "sc_miner_create", "sc_mine", "sc_mine_device", "sc_fast_nms", "sc_decode_jpeg_gray", "sc_imread_gray",
            "sc_last_error", "sc_version")
 
 
@@ -143,6 +143,7 @@ def load_library():
     L.sc_get_timing.argtypes = [vp, P(ctypes.c_double), P(i64)]
     L.sc_miner_create.argtypes = [vp, i32, i32, i32, P(vp)]
     L.sc_mine.argtypes = [vp, vp, i32, i32, i32, vp, vp, i32, P(i32)]
+    L.sc_mine_device.argtypes = [vp, vp, i32, i32, i32, vp, vp, i32, P(i32)]
     L.sc_group_rectangles.argtypes = [vp, i32, i32, ctypes.c_double, vp, i32, P(i32)]
     L.sc_group_detections.argtypes = [vp, i32, i32, i32, ctypes.c_double, vp, i32, vp, P(i32)]
     L.sc_fddb_format.argtypes = [ctypes.c_char_p, vp, i32, ctypes.c_char_p, sz, P(sz)]
@@ -536,3 +537,25 @@ class Miner(Detector):
             _check(rc)
         k = min(n.value, capacity)
         return wins[:k].copy(), (feat[:k].copy() if features else None), n.value
+
+    def mine_device(self, frame, capacity, features=None):
+        """Device frame (uint8 [H, W] tensor) -> (windows, total); the
+        descriptors go into `features` (float32 device tensor holding at least
+        capacity * n_patches * 32 values) when given, never through the host."""
+        if frame.dim() != 2 or frame.element_size() != 1 or not frame.is_cuda or frame.stride(1) != 1:
+            raise ValueError("frame must be a row-major uint8 [H, W] device tensor")
+        H, W = frame.shape
+        if features is not None and (not features.is_cuda or features.element_size() != 4
+                                     or not features.is_contiguous()
+                                     or features.numel() < capacity * self.n_patches * 32):
+            raise ValueError("features must be a contiguous float32 device tensor of "
+                             "capacity * n_patches * 32 values")
+        wins = np.zeros(max(capacity, 1), WINDOW_DTYPE)
+        n = ctypes.c_int()
+        rc = load_library().sc_mine_device(self._h, frame.data_ptr(), W, H, frame.stride(0),
+                                           wins.ctypes.data,
+                                           features.data_ptr() if features is not None else None,
+                                           capacity, ctypes.byref(n))
+        if rc != -6:
+            _check(rc)
+        return wins[:min(n.value, capacity)].copy(), n.value

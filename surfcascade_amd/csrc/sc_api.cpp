@@ -756,7 +756,7 @@ int detect_device_sync(sc_detector *d, const uint8_t *d_frames, int n, int W, in
 // FillNegSamples' scan of one device frame: the shared integral + cascade
 // kernels on the stride-10 grid, then candidate selection and descriptors.
 int mine_sync(sc_detector *d, const uint8_t *d_frame, int W, int H, int stride, sc_window *wins,
-              float *feat, int capacity, int *n_out) {
+              float *feat, int capacity, int *n_out, bool feat_device = false) {
     if (!d->miner) throw Error{SC_ERR_INVALID, "not a miner (sc_miner_create)"};
     if (!d_frame || !n_out || capacity < 0 || (capacity > 0 && !wins))
         throw Error{SC_ERR_INVALID, "bad arguments"};
@@ -804,7 +804,7 @@ int mine_sync(sc_detector *d, const uint8_t *d_frame, int W, int H, int stride, 
     const int kept = (int)std::min<long long>(total, capacity);
     const int P = (int)d->all_rects.size() / 4;
     if (feat && kept > 0) {
-        d->d_feat.ensure((size_t)kept * P * 32);
+        if (!feat_device) d->d_feat.ensure((size_t)kept * P * 32);
         sc::FeatureArgs fa{};
         fa.table = d->d_table.p;
         fa.g = g.tg;
@@ -812,11 +812,12 @@ int mine_sync(sc_detector *d, const uint8_t *d_frame, int W, int H, int stride, 
         fa.n_windows = kept;
         fa.n_patches = P;
         fa.proj_all = d->d_proj_all.p;
-        fa.out = d->d_feat.p;
+        fa.out = feat_device ? feat : d->d_feat.p;
         sc::launch_features(fa, d->stream);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(feat, d->d_feat.p, sizeof(float) * (size_t)kept * P * 32,
-                              hipMemcpyDeviceToHost, d->stream));
+        if (!feat_device)
+            HIPCHK(hipMemcpyAsync(feat, d->d_feat.p, sizeof(float) * (size_t)kept * P * 32,
+                                  hipMemcpyDeviceToHost, d->stream));
     }
     std::vector<sc::MineWindow> mw(kept);
     if (kept > 0)
@@ -1124,6 +1125,16 @@ int sc_mine(sc_detector *d, const uint8_t *gray, int w, int h, int stride, sc_wi
         const uint8_t *fr[1] = {gray};
         upload_frames(d, fr, 1, w, h, stride);
         return mine_sync(d, d->d_frames.p, w, h, w, wins, features, capacity, n_out);
+    });
+}
+
+int sc_mine_device(sc_detector *d, const uint8_t *d_gray, int w, int h, int stride, sc_window *wins,
+                   float *d_features, int capacity, int *n_out) {
+    return guarded([&] {
+        if (!d || !d_gray) throw Error{SC_ERR_INVALID, "bad arguments"};
+        if (w < 2 || h < 2 || stride < w) throw Error{SC_ERR_INVALID, "bad frame geometry"};
+        HIPCHK(hipSetDevice(d->device));
+        return mine_sync(d, d_gray, w, h, stride, wins, d_features, capacity, n_out, true);
     });
 }
 

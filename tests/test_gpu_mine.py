@@ -77,3 +77,19 @@ def test_miner_is_not_a_detector(sc):
     m = sc.Miner(None)
     with pytest.raises(sc.SurfCascadeError):
         m.detect(_frame(200, 200, 1))
+
+
+def test_mine_device_descriptors_stay_on_gpu(sc, oracle):
+    # sc_mine_device: device frame in, descriptors into a device buffer; the
+    # same windows and descriptor bits as sc_mine and the oracle
+    import torch
+    img = _frame(320, 240, 5)
+    m = sc.Miner(None)
+    cap = 64
+    feats = torch.zeros(cap * m.n_patches * 32, dtype=torch.float32, device="cuda:0")
+    wins, n = m.mine_device(torch.from_numpy(img).to("cuda:0"), cap, feats)
+    hw, hf, hn = m.mine(img, cap)
+    assert n == hn and _win(wins) == _win(hw)
+    f = feats.view(cap, m.n_patches, 32)[:len(wins)].cpu().numpy()
+    assert np.array_equal(f.view(np.uint32), hf.view(np.uint32))
+    _check((wins, f, n), oracle.mine(oracle.integral(img), oracle.empty_cascade(), cap))
