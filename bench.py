@@ -25,6 +25,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+# VALU issue ceiling: 256 CUs x 4 SIMDs, a wave64 VALU instruction every 2
+# cycles per SIMD (SIMD-32), 2.4 GHz (MI355X_MICROARCH.md: wave scheduling)
+VALU_ISSUE_PEAK = 1024 * 0.5 * 2.4e9
 
 
 MODELS = os.path.join(ROOT, "surfcascade_amd", "models")
@@ -69,6 +72,10 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--host-steps", type=int, default=5,
                     help="steps of the host-buffer boundary leg (PCIe-inclusive rate; 0: skip)")
+    ap.add_argument("--latency-steps", type=int, default=20,
+                    help="steps of the batch-1 (single-frame) latency leg (0: skip)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="sc_detector_set_option (tuning / A-B runs; never changes results)")
     a = ap.parse_args()
     c = CONFIGS[a.config]
     if a.batch is None and a.shard == "grid":
@@ -82,9 +89,31 @@ def parse():
     return a
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_quota():
+    """CPUs granted by the cgroup quota (cpu.max), or None when unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(frames, model_path, levels, seconds, pedestrian=False):
     """The CPU restatement (oracle/, OpenMP over levels like ObjDetector.cpp:177)
-    on a bounded sample of the same frames: in-memory u8 frame -> raw detections."""
+    on a bounded sample of the same frames: in-memory u8 frame -> raw detections.
+    Timed at every host core this process may run on (sched_getaffinity, no
+    cap: SURVEY.md 8d / BASELINE.md 2) and at 1 thread."""
     from oracle import oracle as O
     O.build()
     if pedestrian:
@@ -99,7 +128,7 @@ def cpu_baseline(frames, model_path, levels, seconds, pedestrian=False):
         ncpu = len(os.sched_getaffinity(0))
     except AttributeError:
         ncpu = os.cpu_count() or 1
-    threads = max(1, min(16, ncpu))
+    threads = max(1, ncpu)
     scratch = np.zeros((H + 1) * (W + 1) * 8, np.float32)
     res = {}
     for nt, budget in ((threads, seconds), (1, seconds)):
@@ -117,7 +146,8 @@ def cpu_baseline(frames, model_path, levels, seconds, pedestrian=False):
             "sample": "%d x %dx%d frames (%d levels, %d grid windows each), integral + adaptive-stride "
                       "detect, %.1f s at %d threads; 1 thread: %.4g windows/s (%d frames, %.1f s)"
                       % (done, W, H, levels, grid, dt, threads, v1, done1, dt1),
-            "value_1thread": v1}
+            "value_1thread": v1, "nproc": os.cpu_count(), "affinity": ncpu,
+            "cgroup_cpu_quota": cpu_quota(), "cpu_model": cpu_model()}
 
 
 def main():
@@ -131,7 +161,7 @@ def main():
     import torch
     import surfcascade_amd as sc
     from surfcascade_amd import synth
-    from surfcascade_amd.dist import gather_detections, merge_records, shard_range
+    from surfcascade_amd.dist import enqueue_and_gather, merge_records, shard_range
 
     torch.cuda.set_device(local_rank)
     dist = None
@@ -149,22 +179,40 @@ def main():
     params = (sc.ScanParams.pedestrian(n_levels=args.levels) if args.pedestrian
               else sc.ScanParams(n_levels=args.levels))
     det = sc.Detector(args.model, params, device=local_rank)
+    opts = {}
+    for o in args.opt:
+        k, v = o.split("=", 1)
+        opts[k] = int(v)
+    det.set_options(**opts)
     if grid_shard:
         det.set_shard(rank, world)
-    cap = 256 * B
-    recs = torch.zeros(cap * sc.RECORD_DTYPE.itemsize, dtype=torch.uint8, device=frames.device)
+    # record buffers: grown (every rank, same size) whenever a scan finds more
+    # detections than they hold -- never truncated (dist.enqueue_and_gather)
     counts = torch.zeros(1 + B, dtype=torch.int32, device=frames.device)
-    gathered = {"counts": [counts], "recs": [recs]}
+    state = {"recs": torch.zeros(256 * B * sc.RECORD_DTYPE.itemsize, dtype=torch.uint8,
+                                 device=frames.device)}
+    gathered = {}
 
     def step():
-        det.enqueue_device(frames, recs, counts)
-        det.synchronize()
-        if dist is not None:  # RCCL gather of the detection records (fixed-size pad)
-            gc, gr = gather_detections(counts, recs)
+        if dist is not None:  # RCCL gather: counts + capacities, then records padded to the max
+            gc, gr, state["recs"] = enqueue_and_gather(det, frames, state["recs"], counts)
             gathered["counts"], gathered["recs"] = gc, gr
+        else:
+            det.enqueue_device(frames, state["recs"], counts)
+            det.synchronize()
 
-    for _ in range(args.warmup):
+    def check_capacity():  # N = 1: the same frames every step -> checked around the timed loop
+        n = int(counts[0].item())
+        if n * sc.RECORD_DTYPE.itemsize > state["recs"].numel():
+            state["recs"] = torch.zeros(n * sc.RECORD_DTYPE.itemsize, dtype=torch.uint8,
+                                        device=frames.device)
+            step()
+        gathered["counts"], gathered["recs"] = [counts.cpu().numpy()], [state["recs"].cpu()]
+
+    for _ in range(max(1, args.warmup)):
         step()
+    if dist is None:
+        check_capacity()
     grid = det.info("grid_windows")
     det.get_timing()  # discard
     det.set_timing(True)
@@ -181,6 +229,22 @@ def main():
     det.set_timing(False)
     kt = det.get_timing()
     visited = det.info("visited")
+    if dist is None:
+        check_capacity()
+    # single-frame latency (C2 names "1080p frame"): batch-1 steps, device-resident
+    lat = None
+    if args.latency_steps > 0 and not grid_shard:
+        one = frames[:1]
+        c1 = torch.zeros(2, dtype=torch.int32, device=frames.device)
+        r1 = torch.zeros(1 << 20, dtype=torch.uint8, device=frames.device)
+        for _ in range(3):
+            det.enqueue_device(one, r1, c1)
+            det.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.latency_steps):
+            det.enqueue_device(one, r1, c1)
+            det.synchronize()
+        lat = (time.perf_counter() - t1) / args.latency_steps
     # the host-buffer boundary (sc_detect_batch: pageable u8 frames in, raw
     # windows out, H2D + D2H over PCIe inside): reported beside, never `value`
     host_dt = None
@@ -211,14 +275,18 @@ def main():
         # whole pipeline (SURVEY.md 8d per-unit figure: W*H + 64 (W+1)(H+1) per frame)
         pipe_bytes = W * H + 64 * (W + 1) * (H + 1)
         pipe_s = sum(v[0] for v in kt.values()) / 1e3 / max(n_win, 1)
-        traffic = None
+        # PMC per launch of the window kernel for this workload (profiles/pmc_windows.json,
+        # written by profiles/pmc_summary.py from the committed rocprofv3 passes)
+        traffic, valu_insts, pmc_src = None, None, None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_windows.json")
-        if os.path.exists(pmc_path):
+        if os.path.exists(pmc_path) and not opts:
             with open(pmc_path) as f:
                 pm = json.load(f)
             if (pm.get("batch") == B and pm.get("width") == W and pm.get("levels") == args.levels
                     and pm.get("config", "C2") == args.config):
                 traffic = pm.get("hbm_bytes_per_launch")
+                valu_insts = pm.get("valu_insts_per_launch")
+                pmc_src = pm.get("source")
         line = {
             "metric": CONFIGS[args.config]["metric"],
             "value": value,
@@ -244,16 +312,31 @@ def main():
                        % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": ("cascade_kernel" if os.environ.get("SC_FULL_GRID", "0") != "0"
-                                    else "chain_kernel"),
+                         "kernel": "cascade_kernel" if opts.get("full_grid") else "chain_kernel",
                          "avg_launch_ms": avg_win_s * 1e3,
                          "bytes_per_launch": tab_bytes * B,
                          "pipeline_achieved": pipe_bytes * B / pipe_s / 1e9,
-                         "pipeline_frac": pipe_bytes * B / pipe_s / 1e9 / HBM_PEAK_GBS},
+                         "pipeline_frac": pipe_bytes * B / pipe_s / 1e9 / HBM_PEAK_GBS,
+                         # beyond-L2 bytes per compulsory byte: re-reads of the table
+                         "traffic_ratio": traffic / (tab_bytes * B) if traffic else None,
+                         # compute side: VALU wave-instructions per launch (PMC
+                         # SQ_INSTS_VALU) over the chip's issue rate (1024 SIMDs x
+                         # 0.5 wave-instr/cycle x 2.4 GHz, MI355X_MICROARCH.md) x
+                         # this launch's time
+                         "valu": (valu_insts / VALU_ISSUE_PEAK / avg_win_s) if valu_insts else None,
+                         "valu_insts_per_launch": valu_insts, "valu_peak_per_s": VALU_ISSUE_PEAK,
+                         "pmc_source": pmc_src},
             "kernel_ms_per_launch": {k: v[0] / max(v[1], 1) for k, v in kt.items()},
             "visited_windows_last_step": visited,
             "detections_last_step": total_det,
         }
+        if lat is not None:
+            line["latency_batch1"] = {
+                "ms_per_frame": lat * 1e3, "value": grid / lat, "unit": "windows/s",
+                "steps": args.latency_steps,
+                "path": "one device-resident frame per step (sc_enqueue_device + synchronize)"}
+        if opts:
+            line["options"] = opts
         if host_dt is not None:
             line["pcie_inclusive"] = {
                 "value": grid * B / host_dt, "unit": "windows/s", "ms_per_step": host_dt * 1e3,

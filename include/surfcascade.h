@@ -125,6 +125,19 @@ int sc_enqueue_device(sc_detector *d, const uint8_t *d_frames, int n, int w,
                       int capacity, int32_t *d_counts);
 int sc_synchronize(sc_detector *d);
 void *sc_detector_stream(sc_detector *d); /* hipStream_t */
+/* Stream ordering of the device-memory entry points (sc_detect_device,
+ * sc_enqueue_device, sc_mine_device).  They run on the detector's own
+ * non-blocking stream, which is NOT ordered against the caller's streams:
+ *  - before handing over device frames / output buffers that work on another
+ *    stream still writes (or frees and re-uses), call
+ *    sc_detector_wait_stream(d, that_stream): the detector's next work waits
+ *    for everything already queued there (no host sync);
+ *  - before reading sc_enqueue_device's outputs on another stream, call
+ *    sc_stream_wait_detector(d, that_stream), or sc_synchronize(d).
+ * Device pointers must be device memory of the detector's GPU (checked:
+ * SC_ERR_INVALID otherwise). */
+int sc_detector_wait_stream(sc_detector *d, void *stream);
+int sc_stream_wait_detector(sc_detector *d, void *stream);
 
 /* ---- hard-negative mining (training side) ----------
  * DenseSURFFeatureExtractor::FillNegSamples' scan of one negative image
@@ -161,6 +174,30 @@ int sc_mine_device(sc_detector *d, const uint8_t *d_gray, int w, int h, int stri
 #define SC_INFO_TABLE_PITCH 4   /* integral-table row pitch in cells         */
 #define SC_INFO_VISITED 5       /* windows the adaptive stride visited (last) */
 int sc_detector_info(sc_detector *d, int what, int64_t *value);
+
+/* ---- tuning and test options ---------------------------------------------
+ * Schedule / layout choices that never change a result bit (the parity tests
+ * run every one of them); the defaults are the measured-fastest.  The library
+ * reads no environment variable: these are set per detector, explicitly. */
+#define SC_OPT_FULL_GRID 1    /* 1: evaluate every grid window (cascade + walk   */
+                              /* kernels) instead of the lazy chain kernel (0) */
+#define SC_OPT_CHUNK_MIN 2    /* stages with >= this many survivors run one lane */
+                              /* per window (0: only stages whose weak count   */
+                              /* exceeds the item buffer)                      */
+#define SC_OPT_TABLE_LAYOUT 3 /* integral cells: 0 channel-split halves,       */
+                              /* 1 interleaved 32-B cells                      */
+#define SC_OPT_PHASES 4       /* phase planes per step: 0 auto (lazy 2, full 1) */
+#define SC_OPT_SUBSTRIPS 5    /* full grid: strips per XCD band (0 auto)       */
+#define SC_OPT_BAND_ROWS 6    /* full grid: grid rows per task band (0: 1)     */
+#define SC_OPT_ROW_ORDER 7    /* chain tasks: 0 level-major, 1 y-major,        */
+                              /* 2 blocks of ROW_BLOCK grid rows (default)     */
+#define SC_OPT_ROW_BLOCK 8    /* grid rows per block (default 32)              */
+#define SC_OPT_CHAIN_CHUNK 9  /* frames per chain-kernel launch at most (0:    */
+                              /* as many as 32-bit table offsets allow)        */
+#define SC_OPT_LDS_WEIGHTS 10 /* -1 auto, 0 weights through the caches, 1 LDS  */
+#define SC_OPT_WGS_PER_CU 11  /* workgroups per CU, 0 = occupancy limit        */
+#define SC_OPT_PROFILE 12     /* chain-kernel phase counters (profiling builds) */
+int sc_detector_set_option(sc_detector *d, int option, int64_t value);
 
 /* Enable per-window debug records (grid order) for the next detect calls. */
 int sc_detector_set_debug(sc_detector *d, int on);

@@ -44,6 +44,16 @@ WINDOW_DTYPE = np.dtype([("level", "<i4"), ("x", "<i4"), ("y", "<i4"), ("w", "<i
                          ("h", "<i4"), ("stage", "<i4"), ("score", "<f8")])
 
 
+# OpenMP threads of the checker: the host's share (at most 16, the GPU box's
+# per-GPU CPU share), overridable per call
+DEFAULT_THREADS = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity")
+                             else (os.cpu_count() or 1)))
+
+
+def _nt(n):
+    return DEFAULT_THREADS if n is None else n
+
+
 def build():
     subprocess.check_call(["make", "-s", "-C", HERE])
 
@@ -91,6 +101,9 @@ def lib():
                                        ctypes.POINTER(ScoModel), ctypes.POINTER(ScoParams),
                                        ctypes.c_void_p, ctypes.c_int64, _i64p, ctypes.c_int, _f32p]
         L.sco_detect_frame.restype = ctypes.c_int64
+        L.sco_walk_grid.argtypes = [_i16p, _f32p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_double, _u8p]
+        L.sco_walk_grid.restype = ctypes.c_int64
         L.sco_mine.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ScoModel), _i32p,
                                ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                ctypes.c_int]
@@ -300,7 +313,7 @@ def empty_cascade(tmpl_w=40, tmpl_h=40):
                    np.zeros(0, np.int32), np.zeros((0, 33), np.float32), np.zeros(0, np.float64))
 
 
-def mine(T, cascade: Cascade, cap, features=True, nthreads=8):
+def mine(T, cascade: Cascade, cap, features=True, nthreads=None):
     """FillNegSamples' scan of one image (sc_oracle.c sco_mine): (candidate
     windows in (level, y, x) order -- the first cap --, their descriptors
     [n, n_patches, 32] over all template patches, total candidate count)."""
@@ -312,12 +325,12 @@ def mine(T, cascade: Cascade, cap, features=True, nthreads=8):
     feat = np.zeros((max(cap, 1), P, 32), np.float32) if features else None
     m = cascade.c()
     n = lib().sco_mine(_p(T, _f32p), W, H, ctypes.byref(m), _p(patches, _i32p), P, out.ctypes.data,
-                       feat.ctypes.data if features else None, cap, nthreads)
+                       feat.ctypes.data if features else None, cap, _nt(nthreads))
     k = min(n, cap)
     return out[:k].copy(), (feat[:k].copy() if features else None), int(n)
 
 
-def eval_grid(T, cascade: Cascade, params: Params, nthreads=8):
+def eval_grid(T, cascade: Cascade, params: Params, nthreads=None):
     T = np.ascontiguousarray(T, np.float32)
     H, W = T.shape[0] - 1, T.shape[1] - 1
     n = grid_count(W, H, params)
@@ -325,25 +338,25 @@ def eval_grid(T, cascade: Cascade, params: Params, nthreads=8):
     s = np.zeros(n, np.float32)
     m = cascade.c()
     lib().sco_eval_grid(_p(T, _f32p), W, H, ctypes.byref(m), ctypes.byref(params.c()),
-                        _p(p, _i16p), _p(s, _f32p), nthreads)
+                        _p(p, _i16p), _p(s, _f32p), _nt(nthreads))
     return p, s
 
 
-def detect(T, cascade: Cascade, params: Params, nthreads=8):
+def detect(T, cascade: Cascade, params: Params, nthreads=None):
     """Reference loop (adaptive stride).  Returns (sorted windows, n_visited)."""
     T = np.ascontiguousarray(T, np.float32)
     H, W = T.shape[0] - 1, T.shape[1] - 1
     m = cascade.c()
     nv = ctypes.c_int64(0)
     n = lib().sco_detect(_p(T, _f32p), W, H, ctypes.byref(m), ctypes.byref(params.c()), None, 0,
-                         ctypes.byref(nv), nthreads)
+                         ctypes.byref(nv), _nt(nthreads))
     out = np.zeros(max(n, 1), WINDOW_DTYPE)
     lib().sco_detect(_p(T, _f32p), W, H, ctypes.byref(m), ctypes.byref(params.c()),
-                     out.ctypes.data, n, ctypes.byref(nv), nthreads)
+                     out.ctypes.data, n, ctypes.byref(nv), _nt(nthreads))
     return out[:n], nv.value
 
 
-def detect_frame(img, cascade: Cascade, params: Params, nthreads=8, cap=1 << 16, scratch=None):
+def detect_frame(img, cascade: Cascade, params: Params, nthreads=None, cap=1 << 16, scratch=None):
     img = np.ascontiguousarray(img, np.uint8)
     H, W = img.shape
     m = cascade.c()
@@ -351,7 +364,7 @@ def detect_frame(img, cascade: Cascade, params: Params, nthreads=8, cap=1 << 16,
     out = np.zeros(cap, WINDOW_DTYPE)
     sp = _p(scratch, _f32p) if scratch is not None else None
     n = lib().sco_detect_frame(_p(img, _u8p), W, H, W, ctypes.byref(m), ctypes.byref(params.c()),
-                               out.ctypes.data, cap, ctypes.byref(nv), nthreads, sp)
+                               out.ctypes.data, cap, ctypes.byref(nv), _nt(nthreads), sp)
     return out[:min(n, cap)], n, nv.value
 
 
@@ -364,7 +377,7 @@ def all_stage_scores(T, cascade: Cascade, l, x, y):
     return out
 
 
-def stage_score_batch(T, cascade: Cascade, l, x, y, stage, nthreads=8):
+def stage_score_batch(T, cascade: Cascade, l, x, y, stage, nthreads=None):
     T = np.ascontiguousarray(T, np.float32)
     W = T.shape[1] - 1
     l = np.ascontiguousarray(l, np.int32)
@@ -373,7 +386,7 @@ def stage_score_batch(T, cascade: Cascade, l, x, y, stage, nthreads=8):
     out = np.zeros(len(l), np.float32)
     m = cascade.c()
     lib().sco_stage_score_batch(_p(T, _f32p), W, ctypes.byref(m), _p(l, _i32p), _p(x, _i32p),
-                                _p(y, _i32p), len(l), stage, _p(out, _f32p), nthreads)
+                                _p(y, _i32p), len(l), stage, _p(out, _f32p), _nt(nthreads))
     return out
 
 
@@ -397,6 +410,17 @@ def prefilter_mask(T, params: Params):
         m = (((v[..., 0] + v[..., 1]) + v[..., 2]) + v[..., 3]) / np.float32(2)
         out.append((m > np.float32(l * lh) * np.float32(params.prefilter_k)).ravel())
     return np.concatenate(out) if out else np.zeros(0, bool)
+
+
+def walk_grid(p_grid, s_grid, layout, n_stages, stride_score=0.5):
+    """walk_rows in C (sco_walk_grid): the visited mask for large grids."""
+    p = np.ascontiguousarray(p_grid, np.int16)
+    s = np.ascontiguousarray(s_grid, np.float32)
+    lay = np.array([(e[3], e[4], e[5]) for e in layout], np.int64).reshape(-1)
+    vis = np.zeros(len(p), np.uint8)
+    lib().sco_walk_grid(_p(p, _i16p), _p(s, _f32p), lay.ctypes.data, len(layout), n_stages,
+                        stride_score, _p(vis, _u8p))
+    return vis.astype(bool), vis.astype(bool) & (p == n_stages)
 
 
 def walk_rows(p_grid, s_grid, layout, n_stages, stride_score=0.5):

@@ -392,6 +392,34 @@ int64_t sco_detect(const float *T, int W, int H, const sco_model *m,
     return n_det;
 }
 
+/* The adaptive-stride x walk (ObjDetector.cpp:185-217) over per-window
+ * results already computed for the whole stride-`step` grid (sco_eval_grid's
+ * output, canonical level / row / x order): visited[g] = 1 for every window
+ * the reference's loop visits.  The same recurrence as sco_detect: after a
+ * prefilter reject or a final score < stride_score the chain skips a window.
+ * layout: per level (nx, ny, grid base).  Returns the visited count. */
+int64_t sco_walk_grid(const int16_t *p_grid, const float *s_grid, const int64_t *layout,
+                      int n_levels, int n_stages, double stride_score, uint8_t *visited) {
+    int64_t nv = 0;
+    for (int i = 0; i < n_levels; i++) {
+        const int64_t nx = layout[3 * i], ny = layout[3 * i + 1], base = layout[3 * i + 2];
+        for (int64_t r = 0; r < ny; r++) {
+            const int64_t o = base + r * nx;
+            for (int64_t j = 0; j < nx;) {
+                visited[o + j] = 1;
+                nv++;
+                const int pr = p_grid[o + j];
+                if (pr < 0) {
+                    j += 2;
+                    continue;
+                }
+                j += final_score(s_grid[o + j], pr, n_stages) < stride_score ? 2 : 1;
+            }
+        }
+    }
+    return nv;
+}
+
 /* In-memory u8 frame -> raw detections (the reference's per-image body,
  * ObjDetector.cpp:165-220, without decode / file I/O). */
 int64_t sco_detect_frame(const uint8_t *img, int W, int H, int stride,

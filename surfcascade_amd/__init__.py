@@ -41,13 +41,20 @@ RECT_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("width", "<i4"), ("height", 
 
 KERNELS = ("rowscan", "colscan", "windows", "walk")
 
+# sc_detector_set_option keys (include/surfcascade.h SC_OPT_*): schedule and
+# layout choices that never change a result bit
+OPTIONS = {"full_grid": 1, "chunk_min": 2, "table_layout": 3, "phases": 4, "substrips": 5,
+           "band_rows": 6, "row_order": 7, "row_block": 8, "chain_chunk": 9, "lds_weights": 10,
+           "wgs_per_cu": 11, "profile": 12}
+
 # every symbol include/surfcascade.h declares
 EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_model_save",
            "sc_model_num_stages", "sc_model_stage", "sc_model_weak", "sc_model_free",
            "sc_extract_patches", "sc_detector_create", "sc_detector_create_from_model",
            "sc_detector_destroy", "sc_detect", "sc_detect_batch", "sc_detect_device",
-           "sc_enqueue_device", "sc_synchronize", "sc_detector_stream", "sc_detector_info",
-           "sc_detector_set_shard", "sc_detector_set_debug", "sc_debug_dump", "sc_set_timing", "sc_get_timing",
+           "sc_enqueue_device", "sc_synchronize", "sc_detector_stream", "sc_detector_wait_stream",
+           "sc_stream_wait_detector", "sc_detector_info",
+           "sc_detector_set_shard", "sc_detector_set_option", "sc_detector_set_debug", "sc_debug_dump", "sc_set_timing", "sc_get_timing",
            "sc_group_rectangles", "sc_group_detections", "sc_fddb_format",
            "sc_miner_create", "sc_mine", "sc_mine_device", "sc_fast_nms", "sc_decode_jpeg_gray", "sc_imread_gray",
            "sc_last_error", "sc_version")
@@ -135,9 +142,12 @@ def load_library():
     L.sc_synchronize.argtypes = [vp]
     L.sc_detector_stream.argtypes = [vp]
     L.sc_detector_stream.restype = vp
+    L.sc_detector_wait_stream.argtypes = [vp, vp]
+    L.sc_stream_wait_detector.argtypes = [vp, vp]
     L.sc_detector_info.argtypes = [vp, i32, P(i64)]
     L.sc_detector_set_debug.argtypes = [vp, i32]
     L.sc_detector_set_shard.argtypes = [vp, i32, i32]
+    L.sc_detector_set_option.argtypes = [vp, i32, i64]
     L.sc_debug_dump.argtypes = [vp, i32, i32, vp, sz]
     L.sc_set_timing.argtypes = [vp, i32]
     L.sc_get_timing.argtypes = [vp, P(ctypes.c_double), P(i64)]
@@ -433,8 +443,27 @@ class Detector:
             raise ValueError("frames must be row-major [n, H, W] (strides %s)" % (frames.stride(),))
         return n, H, W, s1
 
+    def _after_torch(self, *tensors):
+        """Order the detector's stream after the work torch has queued on the
+        current stream of this device (producers of `tensors`, earlier frees):
+        sc_detector_wait_stream, no host sync.  Every tensor must live on the
+        detector's GPU."""
+        import torch
+        for t in tensors:
+            if t is not None and (not t.is_cuda or t.device.index != self.device):
+                raise ValueError("tensor on %s, detector on cuda:%d" % (t.device, self.device))
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        _check(load_library().sc_detector_wait_stream(self._h, s))
+
+    def _before_torch(self):
+        """Order torch's current stream after the detector's queued work."""
+        import torch
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        _check(load_library().sc_stream_wait_detector(self._h, s))
+
     def detect_device(self, frames, capacity=1 << 18):
         n, H, W, rs = self._device_frames(frames)
+        self._after_torch(frames)
         out = np.zeros(capacity, WINDOW_DTYPE)
         counts = (ctypes.c_int * n)()
         _check(load_library().sc_detect_device(self._h, frames.data_ptr(), n, W, H, rs,
@@ -446,11 +475,17 @@ class Detector:
         return res
 
     def enqueue_device(self, frames, out_records, counts):
-        """Async: out_records = torch uint8 [cap*40] (RECORD_DTYPE), counts = int32 [1+n]."""
+        """Async: out_records = torch uint8 [cap*40] (RECORD_DTYPE), counts = int32 [1+n].
+        Stream-ordered like a torch op on the current stream: the scan waits for
+        the work already queued there, and later work there waits for the scan."""
         n, H, W, rs = self._device_frames(frames)
+        if counts.dtype != __import__("torch").int32 or counts.numel() < 1 + n:
+            raise ValueError("counts must be an int32 tensor of at least 1 + n values")
+        self._after_torch(frames, out_records, counts)
         cap = out_records.numel() * out_records.element_size() // RECORD_DTYPE.itemsize
         _check(load_library().sc_enqueue_device(self._h, frames.data_ptr(), n, W, H, rs,
                                                 out_records.data_ptr(), cap, counts.data_ptr()))
+        self._before_torch()
 
     def synchronize(self):
         _check(load_library().sc_synchronize(self._h))
@@ -468,6 +503,16 @@ class Detector:
 
     def set_debug(self, on=True):
         _check(load_library().sc_detector_set_debug(self._h, int(on)))
+
+    def set_option(self, name, value):
+        """sc_detector_set_option: a tuning / test choice (OPTIONS) for this detector."""
+        _check(load_library().sc_detector_set_option(self._h, OPTIONS[name], int(value)))
+        return self
+
+    def set_options(self, **kw):
+        for k, v in kw.items():
+            self.set_option(k, v)
+        return self
 
     def set_shard(self, rank, world):
         """Window-grid sharding (sc_detector_set_shard): evaluate only the
@@ -550,6 +595,7 @@ class Miner(Detector):
                                      or features.numel() < capacity * self.n_patches * 32):
             raise ValueError("features must be a contiguous float32 device tensor of "
                              "capacity * n_patches * 32 values")
+        self._after_torch(frame, features)
         wins = np.zeros(max(capacity, 1), WINDOW_DTYPE)
         n = ctypes.c_int()
         rc = load_library().sc_mine_device(self._h, frame.data_ptr(), W, H, frame.stride(0),

@@ -120,6 +120,13 @@ struct sc_detector {
     DevBuf<int4> d_rects;         // per weak: template rect record (sc::InlinePatch)
     int chunk_min = 1 << 30;  // one-lane-per-window stages only when n > item buffer
     bool lazy = true;         // chain kernel: only windows the x chain reaches are evaluated
+    int cus = 0;              // compute units of `device` (queried once at creation)
+    // tuning / test options (sc_detector_set_option; never read from the environment)
+    struct Options {
+        int full_grid = 0, chunk_min = 0, table_layout = 0, phases = 0, substrips = 0;
+        int band_rows = 0, row_order = 2, row_block = 32, chain_chunk = 0;
+        int lds_weights = -1, wgs_per_cu = 0, profile = 0;
+    } opt;
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
     Geometry geo;
@@ -231,14 +238,12 @@ void build_geometry(sc_detector *d, int W, int H) {
         // parity-split phase planes: the lazy grid's batches (one parity,
         // windows 2 apart) then read consecutive cells
         // (the full grid -- dumps, the miner -- reads consecutive windows: step planes)
-        const char *ep = std::getenv("SC_PHASES");  // tuning override: 1 or 2 planes per step
-        const int mult = ep ? (std::atoi(ep) == 1 ? 1 : 2) : (d->lazy ? 2 : 1);
+        const int mult = d->opt.phases ? d->opt.phases : (d->lazy ? 2 : 1);  // SC_OPT_PHASES
         t.ph = mult * ng.step;
         const int Q = (W + 1 + t.ph - 1) / t.ph;
         t.Qp = (Q + 15) & ~15;
         t.rowp = 2 * t.ph * t.Qp;
-        const char *el = std::getenv("SC_TABLE_LAYOUT");  // tuning override
-        const bool split = el ? std::atoi(el) == 0 : kSplitLayout;
+        const bool split = d->opt.table_layout ? false : kSplitLayout;  // SC_OPT_TABLE_LAYOUT
         t.cs = split ? 1 : 2;
         t.hs = split ? t.ph * t.Qp : 1;
         t.frame4 = (long long)(H + 1) * t.rowp;
@@ -340,11 +345,9 @@ void build_geometry(sc_detector *d, int W, int H) {
     }
     {   // cascade tasks: one strip (~72 windows wide at the widest level) of a
         // band of band_rows consecutive grid rows of one level
-        const char *e = std::getenv("SC_SUBSTRIPS");  // tuning overrides
-        ng.n_sub = e ? std::max(1, std::atoi(e))
-                     : std::max(1, (ng.nx_max + sc::kXcds * 72 / 2) / (sc::kXcds * 72));
-        const char *eb = std::getenv("SC_BAND_ROWS");
-        ng.band_rows = eb ? std::max(1, std::atoi(eb)) : kBandRows;
+        ng.n_sub = d->opt.substrips ? d->opt.substrips  // SC_OPT_SUBSTRIPS
+                                    : std::max(1, (ng.nx_max + sc::kXcds * 72 / 2) / (sc::kXcds * 72));
+        ng.band_rows = d->opt.band_rows ? d->opt.band_rows : kBandRows;  // SC_OPT_BAND_ROWS
         if (d->shard_world > 1) ng.band_rows = 1;  // a rank's rows are not consecutive
         const int nseg = sc::kXcds * ng.n_sub;
         ng.strip_max = std::max(1, (ng.nx_max + nseg - 1) / nseg);
@@ -389,10 +392,8 @@ void build_geometry(sc_detector *d, int W, int H) {
         // order (0) on the C2 frames; blocks of 64 rows 1 % and of 128 rows
         // 3 % slower than 32 (profiles/r1/sweep); 1: y-major.
         // (The full-grid tasks above are built from the level-major list.)
-        const char *e = std::getenv("SC_ROW_ORDER");  // tuning overrides
-        const int mode = e ? std::atoi(e) : 2;
-        const char *eb = std::getenv("SC_ROW_BLOCK");
-        const int blk = std::max(1, eb ? std::atoi(eb) : 32) * ng.step;
+        const int mode = d->opt.row_order;  // SC_OPT_ROW_ORDER / SC_OPT_ROW_BLOCK
+        const int blk = d->opt.row_block * ng.step;
         if (mode == 1)
             std::stable_sort(ng.rows.begin(), ng.rows.end(),
                              [](const int2 &a, const int2 &b) { return a.y < b.y; });
@@ -483,9 +484,8 @@ void upload_model(sc_detector *d) {
             throw Error{SC_ERR_MODEL, "template patch is not 2x2, 1x4 or 4x1 cells"};
         rects[k] = make_int4(r[0], r[1], wide ? r[3] : r[2], ratio == 1 ? 0 : (wide ? 2 : 1));
     }
-    if (const char *e = std::getenv("SC_CHUNK_MIN")) d->chunk_min = std::max(1, std::atoi(e));
-    if (const char *e = std::getenv("SC_FULL_GRID")) d->lazy = std::atoi(e) == 0;  // A/B, dumps
-    if (d->miner) d->lazy = false;  // FillNegSamples evaluates every window
+    d->chunk_min = d->opt.chunk_min > 0 ? d->opt.chunk_min : 1 << 30;  // SC_OPT_CHUNK_MIN
+    d->lazy = !d->opt.full_grid && !d->miner;  // FillNegSamples evaluates every window
     d->d_w.ensure(w.size());
     d->d_bias.ensure(bias.size());
     d->d_theta.ensure(theta.size());
@@ -534,6 +534,7 @@ sc_detector *make_detector(const sc::Cascade &c, const sc_scan_params *p, int de
         d->casc = c;
         d->miner = miner;
         if (miner) d->all_rects = sc::extract_patches(prm.tmpl_w, prm.tmpl_h);
+        HIPCHK(hipDeviceGetAttribute(&d->cus, hipDeviceAttributeMultiprocessorCount, device));
         HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         upload_model(d);
     } catch (...) {
@@ -553,6 +554,10 @@ void ensure_buffers(sc_detector *d, int n) {
     d->d_st_p.ensure(std::max<size_t>((size_t)g.grid * n, 1));
     d->d_st_s.ensure(std::max<size_t>((size_t)g.grid * n, 1));
     if (d->debug) d->d_dbg_v.ensure(std::max<size_t>((size_t)g.grid * n, 1));
+}
+
+sc::LaunchCfg launch_cfg(const sc_detector *d) {
+    return sc::LaunchCfg{d->cus, d->opt.lds_weights, d->opt.wgs_per_cu};
 }
 
 void timed_begin(sc_detector *d, hipEvent_t *a) {
@@ -618,7 +623,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     const bool lazy = d->lazy && sc::chain_lds_bytes(d->K, seg_max, g.n_levels) <= 160 * 1024;
     if (!lazy) {
         timed_begin(d, &e0);
-        sc::launch_cascade(ca, d->device, d->stream);
+        sc::launch_cascade(ca, launch_cfg(d), d->stream);
         HIPCHK(hipGetLastError());
         timed_end(d, SC_KERNEL_WINDOWS, e0);
     }
@@ -645,8 +650,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
         const size_t n_rows = g.rows.size();
         // table offsets are 32-bit byte offsets from the chunk's first frame
         int chunk = (int)std::max<long long>(1, (1ll << 28) / g.tg.frame4);
-        if (const char *e = std::getenv("SC_CHAIN_CHUNK"))  // testing: smaller frame chunks
-            chunk = std::max(1, std::min(chunk, std::atoi(e)));
+        if (d->opt.chain_chunk > 0) chunk = std::min(chunk, d->opt.chain_chunk);  // SC_OPT_CHAIN_CHUNK
         d->d_entry.ensure(n_rows * std::min(chunk, n) * sc::kXcds + 1);
         if (d->debug) {  // dumps: unevaluated windows read -2, unvisited 0
             HIPCHK(hipMemsetAsync(d->d_st_p.p, 0xFE, (size_t)g.grid * n, d->stream));
@@ -669,7 +673,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             d->err_word = (long long)(n_rows * std::min(chunk, n) * sc::kXcds);
             wc.err = d->d_entry.p + d->err_word;
             wc.frame0 = f0;
-            if (std::getenv("SC_PROF_CHAIN")) {  // profiling builds: cumulative phase cycles
+            if (d->opt.profile) {  // SC_OPT_PROFILE (SC_PROF_CHAIN builds): cumulative phase cycles
                 if (!d->d_prof.p) {
                     d->d_prof.ensure(16);
                     HIPCHK(hipMemsetAsync(d->d_prof.p, 0, 16 * sizeof(unsigned long long), d->stream));
@@ -680,7 +684,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             if (f0 > 0)
                 HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kQueueWords,
                                       d->stream));
-            sc::launch_chain(cc, wc, d->device, d->stream);
+            sc::launch_chain(cc, wc, launch_cfg(d), d->stream);
             HIPCHK(hipGetLastError());
         }
         timed_end(d, SC_KERNEL_WINDOWS, e0);
@@ -706,6 +710,24 @@ void check_chain(sc_detector *d) {
                      "surv %llu need %llu pass %llu\n", pc[0], pc[1], pc[2], pc[3], pc[4], pc[5], pc[6],
                      pc[7], pc[8], pc[9], pc[10], pc[11], pc[12], pc[13], pc[14], pc[15]);
     }
+}
+
+// A caller's device pointer must be device memory of this detector's GPU: a
+// host pointer or another GPU's memory would fault in a kernel instead of
+// returning SC_ERR_INVALID.
+void check_device_ptr(const sc_detector *d, const void *p, const char *what) {
+    if (!p) return;
+    hipPointerAttribute_t at{};
+    const hipError_t e = hipPointerGetAttributes(&at, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // an unregistered host pointer: clear the error
+        throw Error{SC_ERR_INVALID, std::string(what) + " is not device memory"};
+    }
+    if (at.type != hipMemoryTypeDevice && at.type != hipMemoryTypeManaged)
+        throw Error{SC_ERR_INVALID, std::string(what) + " is not device memory"};
+    if (at.device != d->device)
+        throw Error{SC_ERR_INVALID, std::string(what) + " is on device " + std::to_string(at.device) +
+                                        ", the detector on device " + std::to_string(d->device)};
 }
 
 bool rec_less(const sc_det_record &a, const sc_det_record &b) {
@@ -1091,11 +1113,36 @@ void sc_detector_destroy(sc_detector *d) { delete d; }
 
 void *sc_detector_stream(sc_detector *d) { return d ? (void *)d->stream : nullptr; }
 
+int sc_detector_wait_stream(sc_detector *d, void *stream) {
+    return guarded([&] {
+        if (!d) throw Error{SC_ERR_INVALID, "null detector"};
+        HIPCHK(hipSetDevice(d->device));
+        hipEvent_t e = d->ev();
+        HIPCHK(hipEventRecord(e, static_cast<hipStream_t>(stream)));
+        HIPCHK(hipStreamWaitEvent(d->stream, e, 0));
+        d->event_pool.push_back(e);  // reusable once recorded and waited on
+        return SC_OK;
+    });
+}
+
+int sc_stream_wait_detector(sc_detector *d, void *stream) {
+    return guarded([&] {
+        if (!d) throw Error{SC_ERR_INVALID, "null detector"};
+        HIPCHK(hipSetDevice(d->device));
+        hipEvent_t e = d->ev();
+        HIPCHK(hipEventRecord(e, d->stream));
+        HIPCHK(hipStreamWaitEvent(static_cast<hipStream_t>(stream), e, 0));
+        d->event_pool.push_back(e);
+        return SC_OK;
+    });
+}
+
 int sc_detect_device(sc_detector *d, const uint8_t *d_frames, int n, int w, int h, int stride,
                      sc_window *out, int capacity, int *n_out) {
     return guarded([&] {
         if (!d) throw Error{SC_ERR_INVALID, "null detector"};
         HIPCHK(hipSetDevice(d->device));
+        check_device_ptr(d, d_frames, "d_frames");
         return detect_device_sync(d, d_frames, n, w, h, stride, out, capacity, n_out);
     });
 }
@@ -1134,6 +1181,8 @@ int sc_mine_device(sc_detector *d, const uint8_t *d_gray, int w, int h, int stri
         if (!d || !d_gray) throw Error{SC_ERR_INVALID, "bad arguments"};
         if (w < 2 || h < 2 || stride < w) throw Error{SC_ERR_INVALID, "bad frame geometry"};
         HIPCHK(hipSetDevice(d->device));
+        check_device_ptr(d, d_gray, "d_gray");
+        check_device_ptr(d, d_features, "d_features");
         return mine_sync(d, d_gray, w, h, stride, wins, d_features, capacity, n_out, true);
     });
 }
@@ -1163,6 +1212,9 @@ int sc_enqueue_device(sc_detector *d, const uint8_t *d_frames, int n, int w, int
         if (w < 2 || h < 2 || stride < w) throw Error{SC_ERR_INVALID, "bad frame geometry"};
         if (d->miner) throw Error{SC_ERR_INVALID, "a miner scans with sc_mine, not sc_enqueue_device"};
         HIPCHK(hipSetDevice(d->device));
+        check_device_ptr(d, d_frames, "d_frames");
+        check_device_ptr(d, d_out, "d_out");
+        check_device_ptr(d, d_counts, "d_counts");
         enqueue(d, d_frames, n, w, h, stride, d_out, capacity, d_counts);
         return SC_OK;
     });
@@ -1213,6 +1265,39 @@ int sc_detector_set_shard(sc_detector *d, int rank, int world) {
         d->geo.W = d->geo.H = 0;  // rebuild the row list at the next detect
     }
     return SC_OK;
+}
+
+int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
+    if (!d) return fail(SC_ERR_INVALID, "null detector");
+    auto range = [&](int64_t lo, int64_t hi) {
+        if (value < lo || value > hi)
+            throw Error{SC_ERR_INVALID, "option " + std::to_string(option) + " value " +
+                                            std::to_string(value) + " out of range"};
+        return (int)value;
+    };
+    return guarded([&] {
+        sc_detector::Options &o = d->opt;
+        bool regeo = true;  // the geometry / task tables depend on the option
+        switch (option) {
+            case SC_OPT_FULL_GRID: o.full_grid = range(0, 1); break;
+            case SC_OPT_CHUNK_MIN: o.chunk_min = range(0, 1 << 30); regeo = false; break;
+            case SC_OPT_TABLE_LAYOUT: o.table_layout = range(0, 1); break;
+            case SC_OPT_PHASES: o.phases = range(0, 2); break;
+            case SC_OPT_SUBSTRIPS: o.substrips = range(0, 64); break;
+            case SC_OPT_BAND_ROWS: o.band_rows = range(0, 64); break;
+            case SC_OPT_ROW_ORDER: o.row_order = range(0, 2); break;
+            case SC_OPT_ROW_BLOCK: o.row_block = range(1, 1 << 16); break;
+            case SC_OPT_CHAIN_CHUNK: o.chain_chunk = range(0, 1 << 20); regeo = false; break;
+            case SC_OPT_LDS_WEIGHTS: o.lds_weights = range(-1, 1); regeo = false; break;
+            case SC_OPT_WGS_PER_CU: o.wgs_per_cu = range(0, 4); regeo = false; break;
+            case SC_OPT_PROFILE: o.profile = range(0, 1); regeo = false; break;
+            default: throw Error{SC_ERR_INVALID, "unknown option " + std::to_string(option)};
+        }
+        d->chunk_min = o.chunk_min > 0 ? o.chunk_min : 1 << 30;
+        d->lazy = !o.full_grid && !d->miner;
+        if (regeo) d->geo.W = d->geo.H = 0;  // rebuilt at the next detect
+        return SC_OK;
+    });
 }
 
 int sc_detector_set_debug(sc_detector *d, int on) {

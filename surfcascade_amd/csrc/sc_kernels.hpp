@@ -209,13 +209,21 @@ void launch_features(const FeatureArgs &a, hipStream_t s);
 // integral pass 1 (rowcarry) and pass 2 (colstrip), sc_integral.hip
 void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s);
 void launch_colscan(const RowScanArgs &a, int n_frames, hipStream_t s);
+// Per-detector launch configuration: the device's CU count (queried once
+// per detector, no process-wide cache) and the SC_OPT_* launch options.
+struct LaunchCfg {
+    int cus;
+    int lds_weights;  // -1 auto, 0 off, 1 on (when the model fits)
+    int wgs_per_cu;   // 0: occupancy limit
+};
+
 // returns the number of workgroups launched
-int launch_cascade(const CascadeArgs &a, int device, hipStream_t s);
+int launch_cascade(const CascadeArgs &a, const LaunchCfg &c, hipStream_t s);
 void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s);
 // Lazy grid: the walk drives the cascade (chain kernel, sc_windows.hip); the
 // cascade args' st_p / st_s, when not null, receive the evaluated windows
 // (others keep the caller's fill).  Returns the number of workgroups.
-int launch_chain(const CascadeArgs &a, const WalkArgs &w, int device, hipStream_t s);
+int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hipStream_t s);
 size_t chain_lds_bytes(int K, int seg_max, int n_levels);
 size_t cascade_lds_bytes(int K, int strip_max, int band_rows);
 

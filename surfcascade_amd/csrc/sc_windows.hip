@@ -29,7 +29,6 @@
 
 #include <algorithm>
 #include <type_traits>
-#include <cstdlib>
 #include <cfloat>
 #include <cstdint>
 
@@ -1016,28 +1015,22 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
 
 }  // namespace
 
-int launch_cascade(const CascadeArgs &a, int device, hipStream_t s) {
+int launch_cascade(const CascadeArgs &a, const LaunchCfg &c, hipStream_t s) {
     const int SA = (a.strip_max * a.band_rows + 63) & ~63;
     const size_t scratch = kWavesPerWg * wave_scratch_bytes(SA);
     // weights in LDS whenever they fit: measured faster even where it costs
     // occupancy (64x128 model, K = 380: 2 instead of 3 workgroups per CU, -2.5%)
     bool lw = model_lds_bytes(a.K, true) + scratch <= 160 * 1024;
-    if (const char *e = std::getenv("SC_LDS_WEIGHTS")) lw = std::atoi(e) != 0;  // tuning override
+    if (c.lds_weights >= 0) lw = lw && c.lds_weights != 0;  // SC_OPT_LDS_WEIGHTS
     const size_t lds = model_lds_bytes(a.K, lw) + scratch;
-    static int cus = 0, dev_cached = -1;
-    if (dev_cached != device) {
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-        dev_cached = device;
-    }
     int per_cu = 0;
     if (lw)
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cascade_kernel<true>, kCascadeThreads, lds);
     else
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cascade_kernel<false>, kCascadeThreads, lds);
     per_cu = std::max(1, std::min(per_cu, 4));
-    if (const char *e = std::getenv("SC_WGS_PER_CU"))  // tuning override
-        per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
-    const int grid = std::max(1, cus) * per_cu;
+    if (c.wgs_per_cu > 0) per_cu = std::min(per_cu, c.wgs_per_cu);  // SC_OPT_WGS_PER_CU
+    const int grid = std::max(1, c.cus) * per_cu;
     if (lw)
         hipLaunchKernelGGL(cascade_kernel<true>, dim3(grid), dim3(kCascadeThreads), lds, s, a);
     else
@@ -1049,25 +1042,19 @@ void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s) {
     hipLaunchKernelGGL(walk_kernel, dim3(a.n_rows * n_frames), dim3(64), 0, s, a);
 }
 
-int launch_chain(const CascadeArgs &a, const WalkArgs &w, int device, hipStream_t s) {
+int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hipStream_t s) {
     const size_t scratch = kChainWaves * chain_wave_bytes(w.row_max) + w.n_levels * sizeof(LevelInfo);
     bool lw = model_lds_bytes(a.K, true) + scratch <= 160 * 1024;
-    if (const char *e = std::getenv("SC_LDS_WEIGHTS")) lw = std::atoi(e) != 0;  // tuning override
+    if (c.lds_weights >= 0) lw = lw && c.lds_weights != 0;  // SC_OPT_LDS_WEIGHTS
     const size_t lds = model_lds_bytes(a.K, lw) + scratch;
-    static int cus = 0, dev_cached = -1;
-    if (dev_cached != device) {
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-        dev_cached = device;
-    }
     int per_cu = 0;
     if (lw)
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<true>, kChainThreads, lds);
     else
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<false>, kChainThreads, lds);
     per_cu = std::max(1, std::min(per_cu, 4));
-    if (const char *e = std::getenv("SC_WGS_PER_CU"))  // tuning override
-        per_cu = std::max(1, std::min(per_cu, std::atoi(e)));
-    const int grid = std::max(1, cus) * per_cu;
+    if (c.wgs_per_cu > 0) per_cu = std::min(per_cu, c.wgs_per_cu);  // SC_OPT_WGS_PER_CU
+    const int grid = std::max(1, c.cus) * per_cu;
     if (lw)
         hipLaunchKernelGGL(chain_kernel<true>, dim3(grid), dim3(kChainThreads), lds, s, a, w);
     else

@@ -2,9 +2,14 @@
 
 Frames are independent, so a batch shards over ranks with no data-path
 exchange (C3); a single frame shards by (level, y) rows of its window grid
-(Detector.set_shard, every rank rebuilds the integral table); the only collective is the gather of the raw detection records at
-the end: one all_gather of the per-frame counts and one all_gather of a
-fixed-capacity record buffer (RCCL over xGMI on GPUs, gloo in CPU tests).
+(Detector.set_shard, every rank rebuilds the integral table).  The only
+collective is the gather of the raw detection records at the end, in the
+order SURVEY.md 8e gives: one all_gather of the per-frame counts, then one
+all_gather of every rank's records padded to the largest count (RCCL over
+xGMI on GPUs, gloo in CPU tests).  A rank whose device buffer overflowed
+(count > capacity: sc_enqueue_device dropped records) is an error on every
+rank, never a silent truncation; `enqueue_and_gather` re-runs the scan with
+a large enough buffer instead.
 Records (RECORD_DTYPE, 40 B) are unsorted on the device; merge_records()
 returns them in canonical (global frame, level, y, x) order.
 """
@@ -13,6 +18,15 @@ from __future__ import annotations
 import numpy as np
 
 from . import RECORD_DTYPE
+
+
+class RecordOverflow(RuntimeError):
+    """A rank's detection count exceeds its record buffer's capacity."""
+
+    def __init__(self, rank, count, capacity):
+        super().__init__("rank %d found %d detections but its record buffer holds %d"
+                         % (rank, count, capacity))
+        self.rank, self.count, self.capacity = rank, count, capacity
 
 
 def shard_range(n_total: int, world: int, rank: int):
@@ -35,26 +49,80 @@ def grid_row_owner(layout, step, world):
     return own
 
 
-def gather_detections(counts, recs, group=None):
-    """all_gather of counts (int32 [1+B]) and records (uint8 [cap*40])."""
+def _capacity(recs):
+    return recs.numel() * recs.element_size() // RECORD_DTYPE.itemsize
+
+
+def _gather_meta(counts, recs, group):
+    """One all_gather of every rank's (counts..., capacity) as int64 ->
+    host array [world, 2 + B]."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    gc = [torch.zeros_like(counts) for _ in range(world)]
-    gr = [torch.zeros_like(recs) for _ in range(world)]
-    dist.all_gather(gc, counts, group=group)
-    dist.all_gather(gr, recs, group=group)
+    meta = torch.cat([counts.to(torch.int64).reshape(-1),
+                      torch.tensor([_capacity(recs)], dtype=torch.int64, device=counts.device)])
+    gm = [torch.zeros_like(meta) for _ in range(world)]
+    dist.all_gather(gm, meta, group=group)
+    return torch.stack(gm).cpu().numpy()  # one device-to-host copy
+
+
+def _gather_records(gm, counts, recs, group):
+    import torch
+    import torch.distributed as dist
+    ns = [int(m[0]) for m in gm]
+    for r, m in enumerate(gm):
+        if ns[r] > int(m[-1]):
+            raise RecordOverflow(r, ns[r], int(m[-1]))
+    nb = max(ns) * RECORD_DTYPE.itemsize  # every rank sends its first max(count) records
+    gr = [torch.zeros(nb, dtype=recs.dtype, device=recs.device) for _ in gm]
+    if nb > 0:
+        dist.all_gather(gr, recs[:nb].contiguous(), group=group)
+    gc = [m[:-1].astype(np.int32) for m in gm]
     return gc, gr
 
 
+def gather_detections(counts, recs, group=None):
+    """counts: int32 [1+B] (counts[0] = this rank's total), recs: uint8
+    [cap*40] record buffer (sc_enqueue_device's outputs, same B on every rank).
+
+    1) all_gather of the counts (and capacities); 2) all_gather of every
+    rank's first max(count) records (padded).  Raises RecordOverflow on every
+    rank when any rank's count exceeds its capacity (its buffer lost records).
+    Returns (per-rank counts, per-rank record bytes)."""
+    return _gather_records(_gather_meta(counts, recs, group), counts, recs, group)
+
+
+def enqueue_and_gather(det, frames, recs, counts, group=None):
+    """One detect step of a rank followed by the gather: scans `frames` into
+    `recs` / `counts` (sc_enqueue_device); when some rank's detections
+    overflowed its buffer, every rank grows its buffer to the largest count
+    and scans again.  Returns (per-rank counts, per-rank records, recs)."""
+    import torch
+    det.enqueue_device(frames, recs, counts)
+    det.synchronize()
+    gm = _gather_meta(counts, recs, group)
+    need = int(gm[:, 0].max())
+    if (gm[:, 0] > gm[:, -1]).any():
+        if need > _capacity(recs):
+            recs = torch.zeros(need * RECORD_DTYPE.itemsize, dtype=torch.uint8, device=recs.device)
+        det.enqueue_device(frames, recs, counts)
+        det.synchronize()
+        gm = _gather_meta(counts, recs, group)
+    gc, gr = _gather_records(gm, counts, recs, group)
+    return gc, gr, recs
+
+
 def merge_records(gathered_counts, gathered_recs, frame_offsets):
-    """Decode every rank's records, shift frames to global indices, sort."""
+    """Decode every rank's records, shift frames to global indices, sort.
+    A rank whose count exceeds the records it sent raises RecordOverflow."""
     out = []
-    for c, r, off in zip(gathered_counts, gathered_recs, frame_offsets):
+    for r, (c, raw, off) in enumerate(zip(gathered_counts, gathered_recs, frame_offsets)):
         c = np.asarray(c.cpu() if hasattr(c, "cpu") else c)
-        raw = np.asarray(r.cpu() if hasattr(r, "cpu") else r, np.uint8)
+        raw = np.asarray(raw.cpu() if hasattr(raw, "cpu") else raw, np.uint8)
         cap = raw.nbytes // RECORD_DTYPE.itemsize
-        n = min(int(c[0]), cap)
+        n = int(c[0])
+        if n > cap:
+            raise RecordOverflow(r, n, cap)
         a = raw[: n * RECORD_DTYPE.itemsize].view(RECORD_DTYPE).copy()
         a["frame"] += off
         out.append(a)

@@ -158,3 +158,107 @@ def test_gloo_grid_shard_gather_equals_single_process(oracle):
     ref = merge_records([np.array([len(a)])], [a.view(np.uint8)], [0])
     assert len(ref) > 20
     assert got.tobytes() == ref.tobytes()
+
+
+class _FakeDetector:
+    """Stands in for a GPU Detector in the gloo test: enqueue_device writes a
+    precomputed (oracle-made, shuffled like the device's atomics) record list
+    into the caller's buffer up to its capacity and the full counts, exactly
+    as sc_enqueue_device does when its capacity is too small."""
+
+    def __init__(self, records, n_frames):
+        from surfcascade_amd import RECORD_DTYPE
+        self.a, self.n_frames, self.calls = records, n_frames, 0
+        self.itemsize = RECORD_DTYPE.itemsize
+
+    def enqueue_device(self, frames, recs, counts):
+        self.calls += 1
+        cap = recs.numel() // self.itemsize
+        k = min(cap, len(self.a))
+        raw = recs.numpy()
+        raw[:k * self.itemsize] = self.a[:k].view(np.uint8)
+        counts.zero_()
+        counts[0] = len(self.a)
+        for f in range(self.n_frames):
+            counts[1 + f] = int((self.a["frame"] == f).sum())
+
+    def synchronize(self):
+        pass
+
+
+def _overflow_worker(rank, world, port, n_frames, out_q):
+    """Rank 0 finds more detections than its first record buffer holds."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle as O
+    from surfcascade_amd import RECORD_DTYPE, synth
+    from surfcascade_amd.dist import (RecordOverflow, enqueue_and_gather, gather_detections,
+                                      merge_records, shard_range)
+    casc = O.cascade_from_cfg(open(FACE_CFG).read())
+    casc.theta[:] = np.float32(0.45 if rank == 0 else 0.6)  # rank 0: many detections
+    params = O.Params(n_levels=2)
+    start, cnt = shard_range(n_frames, world, rank)
+    frames = np.stack([synth.make_frame(320, 240, 500 + start + k) for k in range(cnt)])
+    a = _records_for(O, casc, frames, params, start, np.random.default_rng(rank))
+    fake = _FakeDetector(a, cnt)
+    cap = 8  # far below rank 0's count
+    recs = torch.zeros(cap * RECORD_DTYPE.itemsize, dtype=torch.uint8)
+    counts = torch.zeros(1 + cnt, dtype=torch.int32)
+    # the plain gather refuses (on every rank) instead of dropping records
+    fake.enqueue_device(None, recs, counts)
+    raised = False
+    try:
+        gather_detections(counts, recs)
+    except RecordOverflow as e:
+        raised = e.rank == 0 and e.capacity == cap
+    # enqueue_and_gather grows every rank's buffer and scans again
+    gc, gr, recs2 = enqueue_and_gather(fake, None, recs, counts)
+    offs = [shard_range(n_frames, world, r)[0] for r in range(world)]
+    merged = merge_records(gc, gr, offs)
+    out_q.put((rank, raised, fake.calls, len(a), recs2.numel() // RECORD_DTYPE.itemsize,
+               merged.tobytes()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_gather_overflow_grows_not_truncates(oracle):
+    """counts first, records padded to the largest count; a rank
+    whose record buffer overflowed is an error on every rank (RecordOverflow),
+    and enqueue_and_gather re-scans with a large enough buffer, so the merged
+    result equals the single-process one."""
+    from surfcascade_amd import RECORD_DTYPE, synth
+    from surfcascade_amd.dist import merge_records
+    world, n_frames = 2, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() + 250) % 1000
+    procs = [ctx.Process(target=_overflow_worker, args=(r, world, port, n_frames, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, raised0, calls0, n0, cap0, m0), (_, raised1, calls1, n1, cap1, m1) = res
+    assert raised0 and raised1  # both ranks learn of rank 0's overflow
+    assert n0 > 8 and calls0 == calls1 == 3  # first scan, enqueue_and_gather's scan + rescan
+    assert cap0 == cap1 == max(n0, n1)
+    assert m0 == m1
+    # single-process reference
+    ref = []
+    for r in range(world):
+        casc = oracle.cascade_from_cfg(open(FACE_CFG).read())
+        casc.theta[:] = np.float32(0.45 if r == 0 else 0.6)
+        from surfcascade_amd.dist import shard_range
+        start, cnt = shard_range(n_frames, world, r)
+        frames = np.stack([synth.make_frame(320, 240, 500 + start + k) for k in range(cnt)])
+        a = _records_for(oracle, casc, frames, oracle.Params(n_levels=2), start,
+                         np.random.default_rng(9))
+        ref.append(merge_records([np.array([len(a)])], [a.view(np.uint8)], [start]))
+    ref = np.concatenate(ref)
+    ref = ref[np.lexsort((ref["x"], ref["y"], ref["level"], ref["frame"]))]
+    assert np.frombuffer(m0, RECORD_DTYPE).tobytes() == ref.tobytes()
+    assert len(ref) == n0 + n1

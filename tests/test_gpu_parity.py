@@ -32,18 +32,17 @@ def _det_set(arr):
 @pytest.mark.parametrize("layout", ["0", "1"])
 @pytest.mark.parametrize("W,H,seed", [(640, 480, 1), (1920, 1080, 1000), (257, 131, 7), (2, 2, 3),
                                       (3000, 67, 5)])
-def test_integral_bit_exact(sc, oracle, monkeypatch, W, H, seed, layout):
-    monkeypatch.setenv("SC_TABLE_LAYOUT", layout)
+def test_integral_bit_exact(sc, oracle, W, H, seed, layout):
     img = _frame(W, H, seed)
-    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1))
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1)).set_option("table_layout", int(layout))
     det.detect(img)  # frames smaller than the window: no rows, integral still built
     T = det.dump_integral(W, H)
     ref = oracle.integral(img)
     assert T.view(np.uint32).tobytes() == ref.view(np.uint32).tobytes()
 
 
-def _grid_parity(sc, oracle, cascade, cfg, img, params_sc, params_or):
-    det = sc.Detector(cfg, params_sc)
+def _grid_parity(sc, oracle, cascade, cfg, img, params_sc, params_or, **opts):
+    det = sc.Detector(cfg, params_sc).set_options(**opts)
     det.set_debug(True)
     wins = det.detect(img)
     p, s, v = det.dump_grid()
@@ -51,13 +50,13 @@ def _grid_parity(sc, oracle, cascade, cfg, img, params_sc, params_or):
     rp, rs = oracle.eval_grid(T, cascade, params_or)
     assert len(p) == len(rp)
     # lazy grid (default): only windows the x chain reaches are evaluated (-2
-    # elsewhere); SC_FULL_GRID=1 evaluates all of them
+    # elsewhere); the full_grid option evaluates all of them
     ev = p != -2
     np.testing.assert_array_equal(p[ev], rp[ev])
     assert s[ev].view(np.uint32).tobytes() == rs[ev].view(np.uint32).tobytes()
     H, W = img.shape
     layout, _ = oracle.grid_layout(W, H, params_or)
-    rv, rdm = oracle.walk_rows(rp, rs, layout, cascade.n_stages, params_or.stride_score)
+    rv, rdm = oracle.walk_grid(rp, rs, layout, cascade.n_stages, params_or.stride_score)
     np.testing.assert_array_equal(v, rv)
     assert ev[rv.astype(bool)].all()  # every visited window was evaluated
     ref, nvis = oracle.detect(T, cascade, params_or)
@@ -73,12 +72,10 @@ def test_grid_parity_640x480_single_scale(sc, oracle, face_cascade):
 
 
 @pytest.mark.parametrize("full", [None, "1"])
-def test_grid_parity_1080p_24_levels(sc, oracle, face_cascade, monkeypatch, full):
-    if full:
-        monkeypatch.setenv("SC_FULL_GRID", full)
+def test_grid_parity_1080p_24_levels(sc, oracle, face_cascade, full):
     img = _frame(1920, 1080, 1000)
     _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=24),
-                 oracle.Params(n_levels=24))
+                 oracle.Params(n_levels=24), full_grid=int(full or 0))
 
 
 def test_grid_parity_default_levels_odd_size(sc, oracle, face_cascade):
@@ -90,52 +87,49 @@ def test_grid_parity_default_levels_odd_size(sc, oracle, face_cascade):
     ("1", None, None, None, "1"), ("40", None, "3", "0", "1"), (None, "3", "1", "1", "1"),
     (None, "2", "5", None, "1"), ("1", None, "2", "1", "1"), (None, None, None, "0", None),
     (None, None, None, "1", None), ("1", None, None, None, None), (None, None, None, None, "1")])
-def test_grid_parity_kernel_paths(sc, oracle, face_cascade, monkeypatch, chunk_min, substrips,
+def test_grid_parity_kernel_paths(sc, oracle, face_cascade, chunk_min, substrips,
                                   band_rows, layout, full):
     """The one-lane-per-window stage path (used for stages with more weak
     classifiers than the item buffer holds), other strip splits, band heights
     and both table cell formats give the same bits as the defaults."""
-    for k, v in (("SC_CHUNK_MIN", chunk_min), ("SC_SUBSTRIPS", substrips),
-                 ("SC_BAND_ROWS", band_rows), ("SC_TABLE_LAYOUT", layout), ("SC_FULL_GRID", full)):
-        if v:
-            monkeypatch.setenv(k, v)
+    opts = {k: int(v) for k, v in (("chunk_min", chunk_min), ("substrips", substrips),
+                                   ("band_rows", band_rows), ("table_layout", layout),
+                                   ("full_grid", full)) if v}
     img = _frame(1280, 720, 77)
     _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=8),
-                 oracle.Params(n_levels=8))
+                 oracle.Params(n_levels=8), **opts)
     if layout:
-        det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1))
+        det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1)).set_option("table_layout", int(layout))
         det.detect(img)
         T = det.dump_integral(*img.shape[::-1])
         assert T.view(np.uint32).tobytes() == oracle.integral(img).view(np.uint32).tobytes()
 
 
 @pytest.mark.parametrize("order,block", [("0", None), ("1", None), ("2", "5")])
-def test_chain_row_orders(sc, oracle, face_cascade, monkeypatch, order, block):
+def test_chain_row_orders(sc, oracle, face_cascade, order, block):
     """The chain kernel's task order (level-major, y-major, other row blocks
-    than the default 64) changes the schedule only, never the bits."""
-    monkeypatch.setenv("SC_ROW_ORDER", order)
+    than the default 32) changes the schedule only, never the bits."""
+    opts = {"row_order": int(order)}
     if block:
-        monkeypatch.setenv("SC_ROW_BLOCK", block)
+        opts["row_block"] = int(block)
     img = _frame(1280, 720, 78)
     _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=8),
-                 oracle.Params(n_levels=8))
+                 oracle.Params(n_levels=8), **opts)
 
 
 @pytest.mark.parametrize("lds_weights", [None, "0"])
-def test_pedestrian_64x128(sc, oracle, ped_cascade, monkeypatch, lds_weights):
-    if lds_weights:  # the cache-read weights variant (models too big for the LDS)
-        monkeypatch.setenv("SC_LDS_WEIGHTS", lds_weights)
+def test_pedestrian_64x128(sc, oracle, ped_cascade, lds_weights):
+    # lds_weights 0: the cache-read weights variant (models too big for the LDS)
     img = _frame(960, 540, 21)
     _grid_parity(sc, oracle, ped_cascade, PED_CFG, img,
                  sc.ScanParams.pedestrian(n_levels=12),
-                 oracle.Params(base_len=64, aspect_h=2, n_levels=12))
+                 oracle.Params(base_len=64, aspect_h=2, n_levels=12),
+                 **({"lds_weights": int(lds_weights)} if lds_weights else {}))
 
 
 @pytest.mark.parametrize("full", [None, "1"])
-def test_permissive_cascade_many_detections(sc, oracle, face_cascade, monkeypatch, full):
+def test_permissive_cascade_many_detections(sc, oracle, face_cascade, full):
     """Lowered thetas: many windows reach the last stage (detections + stride 1)."""
-    if full:
-        monkeypatch.setenv("SC_FULL_GRID", full)
     from surfcascade_amd import synth
     c = face_cascade
     theta = np.full(c.n_stages, 0.2, np.float32)
@@ -144,7 +138,7 @@ def test_permissive_cascade_many_detections(sc, oracle, face_cascade, monkeypatc
     casc_sc = sc.Model.parse(text)
     casc_or = oracle.cascade_from_cfg(text)
     img = _frame(640, 480, 2)
-    det = sc.Detector(casc_sc, sc.ScanParams(n_levels=3))
+    det = sc.Detector(casc_sc, sc.ScanParams(n_levels=3)).set_option("full_grid", int(full or 0))
     wins = det.detect(img)
     T = oracle.integral(img)
     ref, nvis = oracle.detect(T, casc_or, oracle.Params(n_levels=3))
@@ -153,17 +147,16 @@ def test_permissive_cascade_many_detections(sc, oracle, face_cascade, monkeypatc
     assert det.info("visited") == nvis
 
 
-def test_lazy_grid_wide_rows_and_frame_chunks(sc, oracle, face_cascade, monkeypatch):
+def test_lazy_grid_wide_rows_and_frame_chunks(sc, oracle, face_cascade):
     """Row segments wider than one 64-window batch per parity (several rounds per
     task) and a batch split into several chain-kernel launches (frame chunks)."""
-    monkeypatch.setenv("SC_CHAIN_CHUNK", "2")
     from surfcascade_amd import synth
     c = face_cascade
     theta = np.full(c.n_stages, 0.3, np.float32)  # many good windows: frequent parity switches
     text = synth.write_cfg(synth.cascade_tree(c.n_weak, theta, c.patch_index, c.w, c.bias))
     casc_or = oracle.cascade_from_cfg(text)
     frames = np.stack([_frame(3000, 160, 700 + k) for k in range(5)])
-    det = sc.Detector(sc.Model.parse(text), sc.ScanParams(n_levels=3))
+    det = sc.Detector(sc.Model.parse(text), sc.ScanParams(n_levels=3)).set_option("chain_chunk", 2)
     batch = det.detect_batch(frames)
     vis = 0
     for k in range(5):
