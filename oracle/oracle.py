@@ -101,6 +101,8 @@ def lib():
                                        ctypes.POINTER(ScoModel), ctypes.POINTER(ScoParams),
                                        ctypes.c_void_p, ctypes.c_int64, _i64p, ctypes.c_int, _f32p]
         L.sco_detect_frame.restype = ctypes.c_int64
+        L.sco_exposure.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ScoModel),
+                                   ctypes.POINTER(ScoParams), _i64p, ctypes.c_int]
         L.sco_walk_grid.argtypes = [_i16p, _f32p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_double, _u8p]
         L.sco_walk_grid.restype = ctypes.c_int64
@@ -410,6 +412,16 @@ def prefilter_mask(T, params: Params):
         m = (((v[..., 0] + v[..., 1]) + v[..., 2]) + v[..., 3]) / np.float32(2)
         out.append((m > np.float32(l * lh) * np.float32(params.prefilter_k)).ravel())
     return np.concatenate(out) if out else np.zeros(0, bool)
+
+
+def exposure(T, cascade: Cascade, params: Params, nthreads=None):
+    """sco_exposure counters (see sc_oracle.c) for one frame's table."""
+    H, W = T.shape[0] - 1, T.shape[1] - 1
+    st = np.zeros(8, np.int64)
+    m = cascade.c()
+    lib().sco_exposure(_p(T, _f32p), W, H, ctypes.byref(m), ctypes.byref(params.c()), _p(st, _i64p),
+                       _nt(nthreads))
+    return st
 
 
 def walk_grid(p_grid, s_grid, layout, n_stages, stride_score=0.5):

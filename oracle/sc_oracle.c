@@ -420,6 +420,85 @@ int64_t sco_walk_grid(const int16_t *p_grid, const float *s_grid, const int64_t 
     return nv;
 }
 
+/* ---- exposure to the unpinned third-party arithmetic -------
+ * Over the windows the reference visits (the sco_detect loop), counts:
+ *  st[0] weak evaluations; st[1] / st[2] those whose f64 sigmoid
+ *  1/(1+exp(-z)) (LogisticRegression.cpp:65) lies within 2 / 16 ulp(f64) of
+ *  an f32 rounding boundary -- where a CRT exp() 1-2 ulp away from glibc's
+ *  could change the (float) cast;
+ *  st[3] stage decisions (ObjDetector.cpp:197), st[4] those with the stage
+ *  score within one f32 ulp of theta;
+ *  st[5] windows with a final score (prefilter passed), st[6] those whose
+ *  final score (s + p + 1)/S lies within one f32 ulp of 0.5 (:214).
+ *  st[7] integral sums above 2^24 among the table's channel values (the
+ *  order-sensitive regime of cv::integral: an IPP route adding in another
+ *  order could differ there). */
+static int near_f32_boundary(double y, int ulps) {
+    float f = (float)y;
+    double lo = (double)nextafterf(f, -INFINITY), hi = (double)nextafterf(f, INFINITY);
+    double m1 = ((double)f + hi) * 0.5, m2 = ((double)f + lo) * 0.5;  /* exact in f64 */
+    double u = nextafter(y, INFINITY) - y;
+    double d = fmin(fabs(y - m1), fabs(y - m2));
+    return d <= ulps * u;
+}
+
+void sco_exposure(const float *T, int W, int H, const sco_model *m, const sco_params *p,
+                  int64_t st[8], int nthreads) {
+    int stp = sco_step(p), nl = sco_effective_levels(W, H, p);
+    const int S = m->n_stages;
+    int64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
+#pragma omp parallel for schedule(dynamic) num_threads(nthreads > 0 ? nthreads : 1) \
+    reduction(+ : a0, a1, a2, a3, a4, a5, a6)
+    for (int i = 0; i < nl; i++) {
+        int l = sco_level_len(p->base_len, i), lh = l * p->aspect_h;
+        float scale = (float)l / (float)m->tmpl_w;
+        for (int y = 0; y <= H - lh; y += stp) {
+            int multi = 1;
+            for (int x = 0; x <= W - l; x += multi * stp) {
+                if (!sco_prefilter(T, W, x, y, l, lh, p->prefilter_k, NULL)) {
+                    multi = 2;
+                    continue;
+                }
+                int pr;
+                float score = 0.0f;
+                int64_t off = 0;
+                for (pr = 0; pr < S; pr++) {
+                    float sum = 0.0f;
+                    for (int k = 0; k < m->n_weak[pr]; k++) {
+                        const float *w = m->w + 33 * (off + k);
+                        int32_t rc[4];
+                        float f[32];
+                        sco_project(m->patch + 4 * (off + k), scale, x, y, rc);
+                        sco_calc_feature(T, W, rc, f);
+                        float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                        for (int q = 0; q < 32; q += 4)
+                            for (int j = 0; j < 4; j++) s4[j] = w[q + j] * f[q + j] + s4[j];
+                        double z = (double)((s4[0] + s4[1]) + (s4[2] + s4[3]));
+                        z += (double)w[32] * m->bias[off + k];
+                        double yv = 1.0 / (1.0 + exp(-z));
+                        a0++;
+                        a1 += near_f32_boundary(yv, 2);
+                        a2 += near_f32_boundary(yv, 16);
+                        sum += (float)yv;
+                    }
+                    score = sum / (float)m->n_weak[pr];
+                    off += m->n_weak[pr];
+                    a3++;
+                    float th = m->theta[pr];
+                    a4 += fabsf(score - th) <= nextafterf(th, INFINITY) - th;
+                    if ((double)score < (double)th) break;
+                }
+                double fin = final_score(score, pr, S);
+                a5++;
+                a6 += fabs(fin - p->stride_score) <= (double)(nextafterf(0.5f, INFINITY) - 0.5f);
+                multi = fin < p->stride_score ? 2 : 1;
+            }
+        }
+    }
+    for (int64_t c = 0; c < (int64_t)(W + 1) * (H + 1) * 8; c++) a7 += T[c] > 16777216.0f;
+    st[0] = a0; st[1] = a1; st[2] = a2; st[3] = a3; st[4] = a4; st[5] = a5; st[6] = a6; st[7] = a7;
+}
+
 /* In-memory u8 frame -> raw detections (the reference's per-image body,
  * ObjDetector.cpp:165-220, without decode / file I/O). */
 int64_t sco_detect_frame(const uint8_t *img, int W, int H, int stride,

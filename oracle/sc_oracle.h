@@ -89,6 +89,8 @@ int64_t sco_detect(const float *T, int W, int H, const sco_model *m,
                    int64_t *n_visited, int nthreads);
 int64_t sco_walk_grid(const int16_t *p_grid, const float *s_grid, const int64_t *layout,
                       int n_levels, int n_stages, double stride_score, uint8_t *visited);
+void sco_exposure(const float *T, int W, int H, const sco_model *m, const sco_params *p,
+                  int64_t st[8], int nthreads);
 int64_t sco_detect_frame(const uint8_t *img, int W, int H, int stride,
                          const sco_model *m, const sco_params *p,
                          sco_window *out, int64_t cap, int64_t *n_visited,

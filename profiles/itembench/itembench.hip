@@ -1,0 +1,233 @@
+// itembench.hip -- microbenchmark of the detect path's inner loop: one
+// (window, weak classifier) item = CalcFeature + Normalize + LR::Predict
+// (DenseSURFFeatureExtractor.cpp:379-457, LogisticRegression.cpp:46-68) over
+// a real item stream (profiles/itembench/run.py builds it from the C2 frame's
+// visited windows in the chain kernel's order).  Variants of the item loop
+// are timed against each other; every variant's outputs must equal the
+// production weak_eval's bit for bit (run.py checks).  Measurement tool only.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../surfcascade_amd/csrc/sc_device.hpp"
+
+using namespace sc;
+
+namespace {
+
+struct Item {
+    unsigned origin;  // float4 offset of the window's origin cell in the frame table
+    unsigned short k;
+    unsigned char level, parity;
+};
+
+struct Args {
+    const float4 *table;
+    TableGeom g;
+    const Item *items;      // per XCD queue: items[q * cap + i]
+    const int *n_items;     // [8]
+    long long cap;
+    const float4 *w;        // [K][9]
+    const double *bias;     // [K]
+    const int4 *rects;      // [K]
+    const float *scale;     // [levels]
+    int K, n_levels;
+    float *out;             // same indexing as items
+    int *tickets;           // [8 * 64]
+    unsigned omask;         // ablation: origin &= omask (0xffffffff: real addresses)
+};
+
+__device__ __forceinline__ unsigned xcc() {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & 7;
+}
+
+__device__ __forceinline__ InlinePatch project(const Args &a, const int4 *R, const float *Sc, const Item &it) {
+    const int4 rc = R[it.k];
+    const float s = Sc[it.level];
+    const int px = (int)((float)rc.x * s), py = (int)((float)rc.y * s), e = (int)((float)rc.z * s);
+    InlinePatch p;
+    p.shape = rc.w;
+    p.c = rc.w == 0 ? (e >> 1) : e;
+    p.row0 = py * a.g.rowp;
+    p.rowstep = p.c * a.g.rowp;
+    p.x0 = it.parity * a.g.step + px;
+    p.cb = a.g.at0((unsigned)(it.parity * a.g.step));
+    p.phm = a.g.phm;
+    p.ph = a.g.ph;
+    p.Qp = a.g.Qp;
+    p.cs = a.g.cs;
+    return p;
+}
+
+constexpr int kChunk = 64;
+constexpr int kBlock = 8;  // chunks per ticket
+
+template <int WAVES>
+__device__ __forceinline__ void stage(const Args &a, unsigned char *smem, float4 *&Wl, double *&Bl, int4 *&Rl,
+                                      float *&Sc) {
+    Wl = reinterpret_cast<float4 *>(smem);
+    Bl = reinterpret_cast<double *>(Wl + a.K * 9);
+    Rl = reinterpret_cast<int4 *>(Bl + a.K);
+    Sc = reinterpret_cast<float *>(Rl + a.K);
+    for (int i = threadIdx.x; i < a.K * 9; i += WAVES * 64) Wl[i] = a.w[i];
+    for (int i = threadIdx.x; i < a.K; i += WAVES * 64) {
+        Bl[i] = a.bias[i];
+        Rl[i] = a.rects[i];
+    }
+    for (int i = threadIdx.x; i < a.n_levels; i += WAVES * 64) Sc[i] = a.scale[i];
+    __syncthreads();
+}
+
+// V0: the production item (weak_eval), one item per lane per iteration.
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_base(Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4 *Wl; double *Bl; int4 *Rl; float *Sc;
+    stage<WAVES>(a, smem, Wl, Bl, Rl, Sc);
+    const int lane = threadIdx.x & 63;
+    const unsigned q0 = xcc();
+    const char *Tb = reinterpret_cast<const char *>(a.table);
+    for (unsigned qi = 0; qi < 8; qi++) {  // own XCD's queue first, then steal
+      const unsigned q = (q0 + qi) & 7;
+      const Item *I = a.items + q * a.cap;
+      float *O = a.out + q * a.cap;
+      const int n = a.n_items[q];
+      for (;;) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&a.tickets[q * 64], 1);
+        b0 = __builtin_amdgcn_readfirstlane(b0) * kChunk * kBlock;
+        if (b0 >= n) break;
+        const int b1 = min(n, b0 + kChunk * kBlock);
+        for (int i = b0 + lane; i < b1; i += 64) {
+            Item it = I[i];
+            it.origin &= a.omask;
+            const TabView T{Tb, it.origin << 4};
+            O[i] = weak_eval(T, a.g.hs, project(a, Rl, Sc, it), Wl + it.k * 9, Bl[it.k]);
+        }
+      }
+    }
+}
+
+// A0 (ablation, wrong results): every lane of a wave evaluates the item of the
+// wave's first lane: the same instruction stream with one cache line per
+// wave-load -- the issue-bound limit of the item loop.
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_bcast(Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4 *Wl; double *Bl; int4 *Rl; float *Sc;
+    stage<WAVES>(a, smem, Wl, Bl, Rl, Sc);
+    const int lane = threadIdx.x & 63;
+    const unsigned q0 = xcc();
+    const char *Tb = reinterpret_cast<const char *>(a.table);
+    for (unsigned qi = 0; qi < 8; qi++) {
+      const unsigned q = (q0 + qi) & 7;
+      const Item *I = a.items + q * a.cap;
+      float *O = a.out + q * a.cap;
+      const int n = a.n_items[q];
+      for (;;) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&a.tickets[q * 64], 1);
+        b0 = __builtin_amdgcn_readfirstlane(b0) * kChunk * kBlock;
+        if (b0 >= n) break;
+        const int b1 = min(n, b0 + kChunk * kBlock);
+        for (int i = b0 + lane; i < b1; i += 64) {
+            Item it = I[i];
+            // the whole item is the first lane's (a window valid for its own
+            // level); lane offsets stay inside the first lane's phase-plane row (patch
+            // columns reach at most l/6 + 1 <= 106 cells further): no access
+            // leaves the table
+            const unsigned o0 = __builtin_amdgcn_readfirstlane(it.origin);
+            unsigned d = (unsigned)(lane & a.omask);
+            if (o0 % (unsigned)a.g.Qp + d + 110u >= (unsigned)a.g.Qp) d = 0;
+            it.origin = o0 + d;
+            it.k = (unsigned short)__builtin_amdgcn_readfirstlane(it.k);
+            it.level = (unsigned char)__builtin_amdgcn_readfirstlane(it.level);
+            it.parity = (unsigned char)__builtin_amdgcn_readfirstlane(it.parity);
+            const TabView T{Tb, it.origin << 4};
+            O[i] = weak_eval(T, a.g.hs, project(a, Rl, Sc, it), Wl + it.k * 9, Bl[it.k]);
+        }
+      }
+    }
+}
+
+// V1: software pipelined: the next item's corner loads are issued right
+// after this item's box sums (uniform 20-load set), so they are in flight
+// during this item's normalise + LR + sigmoid.
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_pipe(Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4 *Wl; double *Bl; int4 *Rl; float *Sc;
+    stage<WAVES>(a, smem, Wl, Bl, Rl, Sc);
+    const int lane = threadIdx.x & 63;
+    const unsigned q0 = xcc();
+    const char *Tb = reinterpret_cast<const char *>(a.table);
+    for (unsigned qi = 0; qi < 8; qi++) {  // own XCD's queue first, then steal
+      const unsigned q = (q0 + qi) & 7;
+      const Item *I = a.items + q * a.cap;
+      float *O = a.out + q * a.cap;
+      const int n = a.n_items[q];
+      for (;;) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&a.tickets[q * 64], 1);
+        b0 = __builtin_amdgcn_readfirstlane(b0) * kChunk * kBlock;
+        if (b0 >= n) break;
+        const int b1 = min(n, b0 + kChunk * kBlock);
+        float4 cn[20];
+        int i = b0 + lane;
+        Item it{};
+        int shape = 0;
+        if (i < b1) {
+            it = I[i];
+            it.origin &= a.omask;
+            const InlinePatch p = project(a, Rl, Sc, it);
+            shape = p.shape;
+            corners_load(TabView{Tb, it.origin << 4}, a.g.hs, p, cn);
+        }
+        for (int c = b0; c < b1; c += 64) {
+            f2 fp[16];
+            corners_box(shape, cn, fp);
+            const int ic = i;
+            const Item itc = it;
+            i = c + 64 + lane;
+            if (i < b1) {
+                it = I[i];
+                it.origin &= a.omask;
+                const InlinePatch p = project(a, Rl, Sc, it);
+                shape = p.shape;
+                corners_load(TabView{Tb, it.origin << 4}, a.g.hs, p, cn);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (ic < b1) {
+                normalize2(fp);
+                O[ic] = lr_predict2(fp, Wl + itc.k * 9, Bl[itc.k]);
+            }
+        }
+      }
+    }
+}
+
+}  // namespace
+
+extern "C" int ib_run(int variant, int waves, const Args *a, void *stream) {
+    const size_t lds = (size_t)a->K * (144 + 8 + 16) + a->n_levels * 4 + 64;
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    hipStream_t s = (hipStream_t)stream;
+    hipMemsetAsync(a->tickets, 0, 8 * 64 * 4, s);
+#define L(KER, WV) hipLaunchKernelGGL((KER<WV>), dim3(cus), dim3(WV * 64), lds, s, *a)
+    if (variant == 0) {
+        if (waves == 8) L(k_base, 8); else if (waves == 12) L(k_base, 12); else if (waves == 16) L(k_base, 16); else return -1;
+    } else if (variant == 1) {
+        if (waves == 8) L(k_pipe, 8); else if (waves == 12) L(k_pipe, 12); else if (waves == 16) L(k_pipe, 16); else return -1;
+    } else if (variant == 2) {
+        if (waves == 8) L(k_bcast, 8); else if (waves == 12) L(k_bcast, 12); else if (waves == 16) L(k_bcast, 16); else return -1;
+    } else {
+        return -1;
+    }
+#undef L
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+extern "C" int ib_args_size() { return (int)sizeof(Args); }
