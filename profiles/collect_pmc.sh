@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 run() {  # run NAME "COUNTERS" [bench args]
   local name=$1 ctr=$2; shift 2
   timeout -k 10 300 rocprofv3 --pmc $ctr --kernel-trace --output-format csv \
-      -d "$R/$OUT/$name" -o pmc -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu --host-steps 0 "$@" \
+      -d "$R/$OUT/$name" -o pmc -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu --host-steps 0 --latency-steps 0 "$@" \
       > "$R/$OUT/$name.json" 2> "$R/$OUT/$name.err"
 }
 run fetch "FETCH_SIZE" "$@" &&

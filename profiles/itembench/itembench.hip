@@ -34,7 +34,8 @@ struct Args {
     int K, n_levels;
     float *out;             // same indexing as items
     int *tickets;           // [8 * 64]
-    unsigned omask;         // ablation: origin &= omask (0xffffffff: real addresses)
+    unsigned omask;         // ablation (k_bcast only): lane offset mask
+    unsigned fold;          // ablation (k_fold only): table row &= fold
 };
 
 __device__ __forceinline__ unsigned xcc() {
@@ -102,7 +103,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_base(Args a) {
         const int b1 = min(n, b0 + kChunk * kBlock);
         for (int i = b0 + lane; i < b1; i += 64) {
             Item it = I[i];
-            it.origin &= a.omask;
             const TabView T{Tb, it.origin << 4};
             O[i] = weak_eval(T, a.g.hs, project(a, Rl, Sc, it), Wl + it.k * 9, Bl[it.k]);
         }
@@ -180,7 +180,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_pipe(Args a) {
         int shape = 0;
         if (i < b1) {
             it = I[i];
-            it.origin &= a.omask;
             const InlinePatch p = project(a, Rl, Sc, it);
             shape = p.shape;
             corners_load(TabView{Tb, it.origin << 4}, a.g.hs, p, cn);
@@ -193,8 +192,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_pipe(Args a) {
             i = c + 64 + lane;
             if (i < b1) {
                 it = I[i];
-                it.origin &= a.omask;
-                const InlinePatch p = project(a, Rl, Sc, it);
+                    const InlinePatch p = project(a, Rl, Sc, it);
                 shape = p.shape;
                 corners_load(TabView{Tb, it.origin << 4}, a.g.hs, p, cn);
             }
@@ -203,6 +201,85 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_pipe(Args a) {
                 normalize2(fp);
                 O[ic] = lr_predict2(fp, Wl + itc.k * 9, Bl[itc.k]);
             }
+        }
+      }
+    }
+}
+
+
+// A3 (ablation, wrong results): the production item with every corner's
+// table row folded into a band of (fold+1) rows (row & fold): the same
+// lanes->lines pattern per wave-instruction, a table footprint the XCD's L2
+// holds -- isolates the cost of the gathers that go beyond L2.
+template <int GW, int GH>
+__device__ __forceinline__ void feat_fold(const char *Tb, unsigned colpart, int y, int py, int c, int x0, int cb,
+                                          const TableGeom &g, unsigned fold, f2 (&fp)[16]) {
+    int col[GW + 1];
+#pragma unroll
+    for (int q = 0; q <= GW; q++) {
+        const unsigned x = (unsigned)(x0 + q * c), qq = __umulhi(x, g.phm);
+        col[q] = (int)(x - qq * (unsigned)g.ph) * g.Qp + (int)qq - cb;
+    }
+    float4 cn[2][GH + 1][GW + 1];
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int r = 0; r <= GH; r++) {
+            const unsigned ro = ((unsigned)(y + py + r * c) & fold) * (unsigned)g.rowp + colpart + h * g.hs;
+#pragma unroll
+            for (int q = 0; q <= GW; q++)
+                cn[h][r][q] = *reinterpret_cast<const float4 *>(Tb + ((ro + col[q]) << 4));
+        }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int r = 0; r < GH; r++)
+#pragma unroll
+            for (int q = 0; q < GW; q++) {
+                const float4 tl = cn[h][r][q], br = cn[h][r + 1][q + 1];
+                const float4 tr = cn[h][r][q + 1], bl = cn[h][r + 1][q];
+                const int o = 4 * (r * GW + q) + 2 * h;
+                fp[o] = (f2{tl.x, tl.y} + f2{br.x, br.y}) - (f2{tr.x, tr.y} + f2{bl.x, bl.y});
+                fp[o + 1] = (f2{tl.z, tl.w} + f2{br.z, br.w}) - (f2{tr.z, tr.w} + f2{bl.z, bl.w});
+            }
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_fold(Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4 *Wl; double *Bl; int4 *Rl; float *Sc;
+    stage<WAVES>(a, smem, Wl, Bl, Rl, Sc);
+    const int lane = threadIdx.x & 63;
+    const unsigned q0 = xcc();
+    const char *Tb = reinterpret_cast<const char *>(a.table);
+    for (unsigned qi = 0; qi < 8; qi++) {
+      const unsigned q = (q0 + qi) & 7;
+      const Item *I = a.items + q * a.cap;
+      float *O = a.out + q * a.cap;
+      const int n = a.n_items[q];
+      for (;;) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&a.tickets[q * 64], 1);
+        b0 = __builtin_amdgcn_readfirstlane(b0) * kChunk * kBlock;
+        if (b0 >= n) break;
+        const int b1 = min(n, b0 + kChunk * kBlock);
+        for (int i = b0 + lane; i < b1; i += 64) {
+            const Item it = I[i];
+            const int y = (int)(it.origin / (unsigned)a.g.rowp);
+            const unsigned colpart = it.origin - (unsigned)y * (unsigned)a.g.rowp;
+            const int4 rc = Rl[it.k];
+            const float s = Sc[it.level];
+            const int px = (int)((float)rc.x * s), py = (int)((float)rc.y * s), e = (int)((float)rc.z * s);
+            const int c = rc.w == 0 ? (e >> 1) : e;
+            const int x0 = it.parity * a.g.step + px;
+            const int cb = a.g.at0((unsigned)(it.parity * a.g.step));
+            f2 fp[16];
+            if (rc.w == 0) feat_fold<2, 2>(Tb, colpart, y, py, c, x0, cb, a.g, a.fold, fp);
+            else if (rc.w == 1) feat_fold<1, 4>(Tb, colpart, y, py, c, x0, cb, a.g, a.fold, fp);
+            else feat_fold<4, 1>(Tb, colpart, y, py, c, x0, cb, a.g, a.fold, fp);
+            normalize2(fp);
+            O[i] = lr_predict2(fp, Wl + it.k * 9, Bl[it.k]);
         }
       }
     }
@@ -223,6 +300,8 @@ extern "C" int ib_run(int variant, int waves, const Args *a, void *stream) {
         if (waves == 8) L(k_pipe, 8); else if (waves == 12) L(k_pipe, 12); else if (waves == 16) L(k_pipe, 16); else return -1;
     } else if (variant == 2) {
         if (waves == 8) L(k_bcast, 8); else if (waves == 12) L(k_bcast, 12); else if (waves == 16) L(k_bcast, 16); else return -1;
+    } else if (variant == 3) {
+        if (waves == 8) L(k_fold, 8); else if (waves == 12) L(k_fold, 12); else if (waves == 16) L(k_fold, 16); else return -1;
     } else {
         return -1;
     }

@@ -34,7 +34,7 @@ class Args(ctypes.Structure):
                 ("n_items", ctypes.c_void_p), ("cap", ctypes.c_longlong), ("w", ctypes.c_void_p),
                 ("bias", ctypes.c_void_p), ("rects", ctypes.c_void_p), ("scale", ctypes.c_void_p),
                 ("K", ctypes.c_int), ("n_levels", ctypes.c_int), ("out", ctypes.c_void_p),
-                ("tickets", ctypes.c_void_p), ("omask", ctypes.c_uint)]
+                ("tickets", ctypes.c_void_p), ("omask", ctypes.c_uint), ("fold", ctypes.c_uint)]
 
 
 ITEM = np.dtype([("origin", "<u4"), ("k", "<u2"), ("level", "u1"), ("parity", "u1")])
@@ -128,7 +128,9 @@ def main():
     ap.add_argument("--nseg", type=int, default=8)
     ap.add_argument("--level-group", type=int, default=0)
     ap.add_argument("--omask", type=lambda x: int(x, 0), default=0xFFFFFFFF,
-                    help="ablation: item origins &= mask (small region: cache-resident)")
+                    help="ablation, variant 2 only: lane offset mask (0: every lane reads lane 0's item)")
+    ap.add_argument("--fold", type=lambda x: int(x, 0), default=0xFFFFFFFF,
+                    help="ablation, variant 3 only: table rows &= fold (a 2^k - 1 band the L2 holds)")
     a = ap.parse_args()
     import torch
     from oracle import oracle as O
@@ -171,7 +173,7 @@ def main():
     L.ib_run.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(Args), ctypes.c_void_p]
     assert L.ib_args_size() == ctypes.sizeof(Args), (L.ib_args_size(), ctypes.sizeof(Args))
     args = Args(tab.data_ptr(), g, d_items.data_ptr(), d_n.data_ptr(), cap, d_w.data_ptr(),
-                d_b.data_ptr(), d_r.data_ptr(), d_s.data_ptr(), K, 24, d_out.data_ptr(), d_t.data_ptr(), a.omask)
+                d_b.data_ptr(), d_r.data_ptr(), d_s.data_ptr(), K, 24, d_out.data_ptr(), d_t.data_ptr(), a.omask, a.fold)
     stream = torch.cuda.current_stream().cuda_stream
     ref = None
     res = {}
