@@ -81,7 +81,8 @@ __device__ __forceinline__ void stage(const Args &a, unsigned char *smem, float4
     __syncthreads();
 }
 
-// V0: the production item (weak_eval), one item per lane per iteration.
+// V0: the production item (weak_eval: uniform loads one half at a time since
+// round 2; V11 is round 1's per-shape load branches), one item per lane.
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64, 1) void k_base(Args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -152,18 +153,40 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_bcast(Args a) {
     }
 }
 
-// V1: software pipelined: the next item's corner loads are issued right
-// after this item's box sums (uniform 20-load set), so they are in flight
-// during this item's normalise + LR + sigmoid.
-template <int WAVES>
-__global__ __launch_bounds__(WAVES * 64, 1) void k_pipe(Args a) {
+
+// Ablations of the item arithmetic (wrong results, timing only): ABL 1 skips
+// Normalize, ABL 2 takes the sigmoid in f32, ABL 3 both.
+template <int ABL>
+__device__ __forceinline__ float item_abl(const TabView &T, int hs, const InlinePatch &pj, const float4 *w4,
+                                          double bias) {
+    f2 fp[16];
+    if (pj.shape == 0) patch_features2<2, 2>(T, pj, hs, fp);
+    else if (pj.shape == 1) patch_features2<1, 4>(T, pj, hs, fp);
+    else patch_features2<4, 1>(T, pj, hs, fp);
+    if (!(ABL & 1)) normalize2(fp);
+    if (ABL & 2) {
+        f2 s01 = f2{0.0f, 0.0f}, s23 = f2{0.0f, 0.0f};
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const float4 wv = w4[i];
+            s01 = f2{wv.x, wv.y} * fp[2 * i] + s01;
+            s23 = f2{wv.z, wv.w} * fp[2 * i + 1] + s23;
+        }
+        const float z = (s01.x + s01.y) + (s23.x + s23.y) + w4[8].x * (float)bias;
+        return 1.0f / (1.0f + __expf(-z));
+    }
+    return lr_predict2(fp, w4, bias);
+}
+
+template <int WAVES, int ABL>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_abl(Args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float4 *Wl; double *Bl; int4 *Rl; float *Sc;
     stage<WAVES>(a, smem, Wl, Bl, Rl, Sc);
     const int lane = threadIdx.x & 63;
     const unsigned q0 = xcc();
     const char *Tb = reinterpret_cast<const char *>(a.table);
-    for (unsigned qi = 0; qi < 8; qi++) {  // own XCD's queue first, then steal
+    for (unsigned qi = 0; qi < 8; qi++) {
       const unsigned q = (q0 + qi) & 7;
       const Item *I = a.items + q * a.cap;
       float *O = a.out + q * a.cap;
@@ -174,38 +197,385 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_pipe(Args a) {
         b0 = __builtin_amdgcn_readfirstlane(b0) * kChunk * kBlock;
         if (b0 >= n) break;
         const int b1 = min(n, b0 + kChunk * kBlock);
-        float4 cn[20];
-        int i = b0 + lane;
-        Item it{};
-        int shape = 0;
-        if (i < b1) {
-            it = I[i];
-            const InlinePatch p = project(a, Rl, Sc, it);
-            shape = p.shape;
-            corners_load(TabView{Tb, it.origin << 4}, a.g.hs, p, cn);
-        }
-        for (int c = b0; c < b1; c += 64) {
-            f2 fp[16];
-            corners_box(shape, cn, fp);
-            const int ic = i;
-            const Item itc = it;
-            i = c + 64 + lane;
-            if (i < b1) {
-                it = I[i];
-                    const InlinePatch p = project(a, Rl, Sc, it);
-                shape = p.shape;
-                corners_load(TabView{Tb, it.origin << 4}, a.g.hs, p, cn);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            if (ic < b1) {
-                normalize2(fp);
-                O[ic] = lr_predict2(fp, Wl + itc.k * 9, Bl[itc.k]);
-            }
+        for (int i = b0 + lane; i < b1; i += 64) {
+            Item it = I[i];
+            const TabView T{Tb, it.origin << 4};
+            O[i] = item_abl<ABL>(T, a.g.hs, project(a, Rl, Sc, it), Wl + it.k * 9, Bl[it.k]);
         }
       }
     }
 }
 
+
+// V4: two lanes per item on the interleaved 32-B-cell table (TableGeom cs 2):
+// lane 2i + h holds half h (channels 4h..4h+3) of item i, so one 16-B load
+// instruction reads both halves of 32 items' corners from the same lines
+// (half the line touches of the channel-split layout for sparse survivors,
+// the same for dense ones).  Normalize's and LR's sequential sums run in
+// both lanes of the pair, each term taken from the lane that holds it
+// (DPP quad_perm [0,0,2,2] / [1,1,3,3]): the reference's order exactly.
+// A trip evaluates 64 items as two 32-item halves, then one f64 sigmoid per
+// lane (lane 2i: item i of the first half, lane 2i+1: of the second).
+__device__ __forceinline__ float from_even(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xA0, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float from_odd(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xF5, 0xF, 0xF, false));
+}
+
+template <int GW, int GH>
+__device__ __forceinline__ void half_feats(const char *Tb, unsigned off, const InlinePatch &pj, f2 (&fh)[8]) {
+    int col[GW + 1];
+#pragma unroll
+    for (int q = 0; q <= GW; q++) col[q] = pj.colq(q);
+    float4 cn[GH + 1][GW + 1];
+#pragma unroll
+    for (int r = 0; r <= GH; r++) {
+        const int ro = pj.row0 + r * pj.rowstep;
+#pragma unroll
+        for (int q = 0; q <= GW; q++)
+            cn[r][q] = *reinterpret_cast<const float4 *>(Tb + (off + ((unsigned)(ro + col[q]) << 4)));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int r = 0; r < GH; r++)
+#pragma unroll
+        for (int q = 0; q < GW; q++) {
+            const float4 tl = cn[r][q], br = cn[r + 1][q + 1], tr = cn[r][q + 1], bl = cn[r + 1][q];
+            const int o = 2 * (r * GW + q);
+            fh[o] = (f2{tl.x, tl.y} + f2{br.x, br.y}) - (f2{tr.x, tr.y} + f2{bl.x, bl.y});
+            fh[o + 1] = (f2{tl.z, tl.w} + f2{br.z, br.w}) - (f2{tr.z, tr.w} + f2{bl.z, bl.w});
+        }
+}
+
+// SS = (((eps + c0) + c1) ... + c7), c_(2 cell + h) in lane h of the pair
+__device__ __forceinline__ float ss_pair(const f2 (&fh)[8]) {
+    float ss = FLT_EPSILON;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const f2 a = fh[2 * c] * fh[2 * c], b = fh[2 * c + 1] * fh[2 * c + 1];
+        const float cc = (a.x + a.y) + (b.x + b.y);
+        ss = ss + from_even(cc);
+        ss = ss + from_odd(cc);
+    }
+    return ss;
+}
+
+// z32 of LogisticRegression::Predict: group i = 2 cell + h lives in lane h
+__device__ __forceinline__ float z_pair(const f2 (&fh)[8], const float4 *w4, int h) {
+    float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const float4 wv = w4[2 * c + h];
+        const f2 t01 = f2{wv.x, wv.y} * fh[2 * c], t23 = f2{wv.z, wv.w} * fh[2 * c + 1];
+        s[0] = s[0] + from_even(t01.x);
+        s[1] = s[1] + from_even(t01.y);
+        s[2] = s[2] + from_even(t23.x);
+        s[3] = s[3] + from_even(t23.y);
+        s[0] = s[0] + from_odd(t01.x);
+        s[1] = s[1] + from_odd(t01.y);
+        s[2] = s[2] + from_odd(t23.x);
+        s[3] = s[3] + from_odd(t23.y);
+    }
+    return (s[0] + s[1]) + (s[2] + s[3]);
+}
+
+__device__ __forceinline__ float half_item(const char *Tb, const Item &it, int h, const InlinePatch &pj,
+                                           const float4 *w4) {
+    f2 fh[8];
+    const unsigned off = (it.origin << 4) + (unsigned)h * 16u;
+    if (pj.shape == 0) half_feats<2, 2>(Tb, off, pj, fh);
+    else if (pj.shape == 1) half_feats<1, 4>(Tb, off, pj, fh);
+    else half_feats<4, 1>(Tb, off, pj, fh);
+    const float theta = 0.35355338f;
+    const float t = sqrtf(ss_pair(fh)) * theta, nt = -t;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        fh[j].x = __builtin_amdgcn_fmed3f(fh[j].x, nt, t);
+        fh[j].y = __builtin_amdgcn_fmed3f(fh[j].y, nt, t);
+    }
+    const float r = 1.0f / sqrtf(ss_pair(fh));
+#pragma unroll
+    for (int j = 0; j < 8; j++) fh[j] = fh[j] * f2{r, r};
+    return z_pair(fh, w4, h);
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_pair(Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4 *Wl; double *Bl; int4 *Rl; float *Sc;
+    stage<WAVES>(a, smem, Wl, Bl, Rl, Sc);
+    const int lane = threadIdx.x & 63, h = lane & 1, ii = lane >> 1;
+    const unsigned q0 = xcc();
+    const char *Tb = reinterpret_cast<const char *>(a.table);
+    for (unsigned qi = 0; qi < 8; qi++) {
+      const unsigned q = (q0 + qi) & 7;
+      const Item *I = a.items + q * a.cap;
+      float *O = a.out + q * a.cap;
+      const int n = a.n_items[q];
+      for (;;) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&a.tickets[q * 64], 1);
+        b0 = __builtin_amdgcn_readfirstlane(b0) * kChunk * kBlock;
+        if (b0 >= n) break;
+        const int b1 = min(n, b0 + kChunk * kBlock);
+        for (int c = b0; c < b1; c += 64) {
+            const int iA = c + ii, iB = c + 32 + ii;
+            const Item itA = I[iA < b1 ? iA : b0], itB = I[iB < b1 ? iB : b0];
+            const float zA = half_item(Tb, itA, h, project(a, Rl, Sc, itA), Wl + itA.k * 9);
+            const float zB = half_item(Tb, itB, h, project(a, Rl, Sc, itB), Wl + itB.k * 9);
+            const int k = h ? itB.k : itA.k, i = h ? iB : iA;
+            double prob = (double)(h ? zB : zA);
+            prob += (double)Wl[k * 9 + 8].x * Bl[k];
+            prob = 1.0 / (1.0 + exp(-prob));
+            if (i < b1) O[i] = (float)prob;
+        }
+      }
+    }
+}
+
+
+// V8: one straight-line set of 20 corner loads for every patch shape (the
+// shapes differ only in per-lane offsets; a 2x2 patch's slot 9 repeats its
+// corner (2,2)): no shape-divergent load branches, so every vector-memory
+// instruction carries all the wave's lanes (the texture addresser costs the
+// same per instruction however few lanes are active).
+__device__ __forceinline__ void uload(const TabView &T, int half_off, const InlinePatch &pj, float4 (&cn)[20]) {
+    int col[5], ro[5];
+#pragma unroll
+    for (int c = 0; c < 5; c++) col[c] = pj.colq(c);
+#pragma unroll
+    for (int r = 0; r < 5; r++) ro[r] = pj.row0 + r * pj.rowstep;
+    const bool sq = pj.shape == 0, tall = pj.shape == 1;
+    int off[10];
+#pragma unroll
+    for (int m = 0; m < 10; m++) {
+        const int o0 = ro[m < 9 ? m / 3 : 2] + col[m < 9 ? m % 3 : 2];
+        const int o1 = ro[m / 2] + col[m % 2];
+        const int o2 = ro[m / 5] + col[m % 5];
+        off[m] = sq ? o0 : (tall ? o1 : o2);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int m = 0; m < 10; m++) cn[h * 10 + m] = T.at(h * half_off + off[m]);
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_uload(Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4 *Wl; double *Bl; int4 *Rl; float *Sc;
+    stage<WAVES>(a, smem, Wl, Bl, Rl, Sc);
+    const int lane = threadIdx.x & 63;
+    const unsigned q0 = xcc();
+    const char *Tb = reinterpret_cast<const char *>(a.table);
+    for (unsigned qi = 0; qi < 8; qi++) {
+      const unsigned q = (q0 + qi) & 7;
+      const Item *I = a.items + q * a.cap;
+      float *O = a.out + q * a.cap;
+      const int n = a.n_items[q];
+      for (;;) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&a.tickets[q * 64], 1);
+        b0 = __builtin_amdgcn_readfirstlane(b0) * kChunk * kBlock;
+        if (b0 >= n) break;
+        const int b1 = min(n, b0 + kChunk * kBlock);
+        for (int c = b0; c < b1; c += 64) {
+            const int i = c + lane;
+            const Item it = I[i < b1 ? i : b0];
+            const InlinePatch pj = project(a, Rl, Sc, it);
+            float4 cn[20];
+            uload(TabView{Tb, it.origin << 4}, a.g.hs, pj, cn);
+            __builtin_amdgcn_sched_barrier(0);
+            f2 fp[16];
+            {
+                float4 c0[10], c1[10];
+#pragma unroll
+                for (int m = 0; m < 10; m++) { c0[m] = cn[m]; c1[m] = cn[10 + m]; }
+                f2 h0[8], h1[8];
+                half_box(pj.shape, c0, h0);
+                half_box(pj.shape, c1, h1);
+#pragma unroll
+                for (int cl = 0; cl < 4; cl++) {
+                    fp[4 * cl] = h0[2 * cl]; fp[4 * cl + 1] = h0[2 * cl + 1];
+                    fp[4 * cl + 2] = h1[2 * cl]; fp[4 * cl + 3] = h1[2 * cl + 1];
+                }
+            }
+            normalize2(fp);
+            const float p = lr_predict2(fp, Wl + it.k * 9, Bl[it.k]);
+            if (i < b1) O[i] = p;
+        }
+      }
+    }
+}
+
+
+// V9: V4's two lanes per item with V8's uniform load set: each lane issues
+// the 10 corner loads of its half, straight-line for every shape.
+template <int GW, int GH>
+__device__ __forceinline__ void ib_half_box(const float4 (&cn)[10], f2 (&fh)[8]) {
+#pragma unroll
+    for (int r = 0; r < GH; r++)
+#pragma unroll
+        for (int q = 0; q < GW; q++) {
+            const float4 tl = cn[r * (GW + 1) + q], br = cn[(r + 1) * (GW + 1) + q + 1];
+            const float4 tr = cn[r * (GW + 1) + q + 1], bl = cn[(r + 1) * (GW + 1) + q];
+            const int o = 2 * (r * GW + q);
+            fh[o] = (f2{tl.x, tl.y} + f2{br.x, br.y}) - (f2{tr.x, tr.y} + f2{bl.x, bl.y});
+            fh[o + 1] = (f2{tl.z, tl.w} + f2{br.z, br.w}) - (f2{tr.z, tr.w} + f2{bl.z, bl.w});
+        }
+}
+
+__device__ __forceinline__ float half_item_u(const char *Tb, const Item &it, int h, const InlinePatch &pj,
+                                             const float4 *w4) {
+    int col[5], ro[5];
+#pragma unroll
+    for (int c = 0; c < 5; c++) col[c] = pj.colq(c);
+#pragma unroll
+    for (int r = 0; r < 5; r++) ro[r] = pj.row0 + r * pj.rowstep;
+    const bool sq = pj.shape == 0, tall = pj.shape == 1;
+    const unsigned base = (it.origin << 4) + (unsigned)h * 16u;
+    float4 cn[10];
+#pragma unroll
+    for (int m = 0; m < 10; m++) {
+        const int o0 = ro[m < 9 ? m / 3 : 2] + col[m < 9 ? m % 3 : 2];
+        const int o1 = ro[m / 2] + col[m % 2];
+        const int o2 = ro[m / 5] + col[m % 5];
+        const int off = sq ? o0 : (tall ? o1 : o2);
+        cn[m] = *reinterpret_cast<const float4 *>(Tb + (base + ((unsigned)off << 4)));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    f2 fh[8];
+    if (sq) ib_half_box<2, 2>(cn, fh);
+    else if (tall) ib_half_box<1, 4>(cn, fh);
+    else ib_half_box<4, 1>(cn, fh);
+    const float theta = 0.35355338f;
+    const float t = sqrtf(ss_pair(fh)) * theta, nt = -t;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        fh[j].x = __builtin_amdgcn_fmed3f(fh[j].x, nt, t);
+        fh[j].y = __builtin_amdgcn_fmed3f(fh[j].y, nt, t);
+    }
+    const float r = 1.0f / sqrtf(ss_pair(fh));
+#pragma unroll
+    for (int j = 0; j < 8; j++) fh[j] = fh[j] * f2{r, r};
+    return z_pair(fh, w4, h);
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_pairu(Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4 *Wl; double *Bl; int4 *Rl; float *Sc;
+    stage<WAVES>(a, smem, Wl, Bl, Rl, Sc);
+    const int lane = threadIdx.x & 63, h = lane & 1, ii = lane >> 1;
+    const unsigned q0 = xcc();
+    const char *Tb = reinterpret_cast<const char *>(a.table);
+    for (unsigned qi = 0; qi < 8; qi++) {
+      const unsigned q = (q0 + qi) & 7;
+      const Item *I = a.items + q * a.cap;
+      float *O = a.out + q * a.cap;
+      const int n = a.n_items[q];
+      for (;;) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&a.tickets[q * 64], 1);
+        b0 = __builtin_amdgcn_readfirstlane(b0) * kChunk * kBlock;
+        if (b0 >= n) break;
+        const int b1 = min(n, b0 + kChunk * kBlock);
+        for (int c = b0; c < b1; c += 64) {
+            const int iA = c + ii, iB = c + 32 + ii;
+            const Item itA = I[iA < b1 ? iA : b0], itB = I[iB < b1 ? iB : b0];
+            const float zA = half_item_u(Tb, itA, h, project(a, Rl, Sc, itA), Wl + itA.k * 9);
+            const float zB = half_item_u(Tb, itB, h, project(a, Rl, Sc, itB), Wl + itB.k * 9);
+            const int k = h ? itB.k : itA.k, i = h ? iB : iA;
+            double prob = (double)(h ? zB : zA);
+            prob += (double)Wl[k * 9 + 8].x * Bl[k];
+            prob = 1.0 / (1.0 + exp(-prob));
+            if (i < b1) O[i] = (float)prob;
+        }
+      }
+    }
+}
+
+
+// V10: V8's uniform loads one half at a time (10 loads, box sums of that
+// half, then the other half's 10 loads): half the corner registers, two
+// memory round trips per item.
+__device__ __forceinline__ void uload_half(const TabView &T, int hoff, const int (&off)[10], float4 (&cn)[10]) {
+#pragma unroll
+    for (int m = 0; m < 10; m++) cn[m] = T.at(hoff + off[m]);
+}
+__device__ __forceinline__ void box_half(int shape, const float4 (&cn)[10], f2 *fh) {
+    if (shape == 0) ib_half_box<2, 2>(cn, *reinterpret_cast<f2(*)[8]>(fh));
+    else if (shape == 1) ib_half_box<1, 4>(cn, *reinterpret_cast<f2(*)[8]>(fh));
+    else ib_half_box<4, 1>(cn, *reinterpret_cast<f2(*)[8]>(fh));
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_uhalf(Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4 *Wl; double *Bl; int4 *Rl; float *Sc;
+    stage<WAVES>(a, smem, Wl, Bl, Rl, Sc);
+    const int lane = threadIdx.x & 63;
+    const unsigned q0 = xcc();
+    const char *Tb = reinterpret_cast<const char *>(a.table);
+    for (unsigned qi = 0; qi < 8; qi++) {
+      const unsigned q = (q0 + qi) & 7;
+      const Item *I = a.items + q * a.cap;
+      float *O = a.out + q * a.cap;
+      const int n = a.n_items[q];
+      for (;;) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&a.tickets[q * 64], 1);
+        b0 = __builtin_amdgcn_readfirstlane(b0) * kChunk * kBlock;
+        if (b0 >= n) break;
+        const int b1 = min(n, b0 + kChunk * kBlock);
+        for (int c = b0; c < b1; c += 64) {
+            const int i = c + lane;
+            const Item it = I[i < b1 ? i : b0];
+            const InlinePatch pj = project(a, Rl, Sc, it);
+            int col[5], ro[5], off[10];
+#pragma unroll
+            for (int q2 = 0; q2 < 5; q2++) col[q2] = pj.colq(q2);
+#pragma unroll
+            for (int r = 0; r < 5; r++) ro[r] = pj.row0 + r * pj.rowstep;
+            const bool sq = pj.shape == 0, tall = pj.shape == 1;
+#pragma unroll
+            for (int m = 0; m < 10; m++) {
+                const int o0 = ro[m < 9 ? m / 3 : 2] + col[m < 9 ? m % 3 : 2];
+                const int o1 = ro[m / 2] + col[m % 2];
+                const int o2 = ro[m / 5] + col[m % 5];
+                off[m] = sq ? o0 : (tall ? o1 : o2);
+            }
+            const TabView T{Tb, it.origin << 4};
+            f2 h0[8], h1[8];
+            {
+                float4 cn[10];
+                uload_half(T, 0, off, cn);
+                __builtin_amdgcn_sched_barrier(0);
+                box_half(pj.shape, cn, h0);
+            }
+            {
+                float4 cn[10];
+                uload_half(T, a.g.hs, off, cn);
+                __builtin_amdgcn_sched_barrier(0);
+                box_half(pj.shape, cn, h1);
+            }
+            // interleave the halves back into the 32-feature order: f[8 cell + 4 h + ch]
+            f2 fp[16];
+#pragma unroll
+            for (int cl = 0; cl < 4; cl++) {
+                fp[4 * cl] = h0[2 * cl];
+                fp[4 * cl + 1] = h0[2 * cl + 1];
+                fp[4 * cl + 2] = h1[2 * cl];
+                fp[4 * cl + 3] = h1[2 * cl + 1];
+            }
+            normalize2(fp);
+            const float p = lr_predict2(fp, Wl + it.k * 9, Bl[it.k]);
+            if (i < b1) O[i] = p;
+        }
+      }
+    }
+}
 
 // A3 (ablation, wrong results): the production item with every corner's
 // table row folded into a band of (fold+1) rows (row & fold): the same
@@ -297,9 +667,25 @@ extern "C" int ib_run(int variant, int waves, const Args *a, void *stream) {
     if (variant == 0) {
         if (waves == 8) L(k_base, 8); else if (waves == 12) L(k_base, 12); else if (waves == 16) L(k_base, 16); else return -1;
     } else if (variant == 1) {
-        if (waves == 8) L(k_pipe, 8); else if (waves == 12) L(k_pipe, 12); else if (waves == 16) L(k_pipe, 16); else return -1;
+        return -1;  // (V1, the software-pipelined item, retired: slower, profiles/r2/itembench.md)
     } else if (variant == 2) {
         if (waves == 8) L(k_bcast, 8); else if (waves == 12) L(k_bcast, 12); else if (waves == 16) L(k_bcast, 16); else return -1;
+    } else if (variant == 9) {
+        if (waves == 8) L(k_pairu, 8); else if (waves == 12) L(k_pairu, 12); else if (waves == 16) L(k_pairu, 16); else return -1;
+    } else if (variant == 10) {
+        if (waves == 8) L(k_uhalf, 8); else if (waves == 12) L(k_uhalf, 12); else if (waves == 16) L(k_uhalf, 16); else return -1;
+    } else if (variant == 8) {
+        if (waves == 8) L(k_uload, 8); else if (waves == 12) L(k_uload, 12); else if (waves == 16) L(k_uload, 16); else return -1;
+    } else if (variant == 4) {
+        if (waves == 8) L(k_pair, 8); else if (waves == 12) L(k_pair, 12); else if (waves == 16) L(k_pair, 16); else return -1;
+    } else if (variant == 11) {  // the round-1 production item: per-shape load branches
+        if (waves != 12) return -1;
+        hipLaunchKernelGGL((k_abl<12, 0>), dim3(cus), dim3(768), lds, s, *a);
+    } else if (variant >= 5 && variant <= 7) {
+        if (waves != 12) return -1;
+        if (variant == 5) hipLaunchKernelGGL((k_abl<12, 1>), dim3(cus), dim3(768), lds, s, *a);
+        else if (variant == 6) hipLaunchKernelGGL((k_abl<12, 2>), dim3(cus), dim3(768), lds, s, *a);
+        else hipLaunchKernelGGL((k_abl<12, 3>), dim3(cus), dim3(768), lds, s, *a);
     } else if (variant == 3) {
         if (waves == 8) L(k_fold, 8); else if (waves == 12) L(k_fold, 12); else if (waves == 16) L(k_fold, 16); else return -1;
     } else {

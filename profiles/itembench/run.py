@@ -50,6 +50,24 @@ def geometry(W, H, step=3):
     return g
 
 
+def geometry_inter(W, H, step=3):
+    """interleaved 32-B cells (TableGeom cs 2, hs 1): float4 (y, x, h) =
+    y*rowp + 2*((x % ph)*Qp + x // ph) + h"""
+    g = geometry(W, H, step)
+    g.cs, g.hs = 2, 1
+    return g
+
+
+def inter_table(T, g):
+    H1, W1, _ = T.shape
+    out = np.zeros((H1, g.rowp, 4), np.float32)
+    x = np.arange(W1)
+    cell = 2 * ((x % g.ph) * g.Qp + x // g.ph)
+    out[:, cell, :] = T[:, :, :4]
+    out[:, cell + 1, :] = T[:, :, 4:]
+    return out
+
+
 def split_table(T, g):
     """Reference interleaved (H+1, W+1, 8) table -> phase-split float4 cells."""
     H1, W1, _ = T.shape
@@ -174,23 +192,34 @@ def main():
     assert L.ib_args_size() == ctypes.sizeof(Args), (L.ib_args_size(), ctypes.sizeof(Args))
     args = Args(tab.data_ptr(), g, d_items.data_ptr(), d_n.data_ptr(), cap, d_w.data_ptr(),
                 d_b.data_ptr(), d_r.data_ptr(), d_s.data_ptr(), K, 24, d_out.data_ptr(), d_t.data_ptr(), a.omask, a.fold)
+    # variant 4: the same items on the interleaved-cell table (origin = y*rowp + 2*col)
+    gi = geometry_inter(T.shape[1] - 1, T.shape[0] - 1)
+    tab_i = torch.from_numpy(inter_table(T, gi)).to(dev)
+    items_i = items.copy()
+    yy = items_i["origin"] // g.rowp
+    items_i["origin"] = yy * g.rowp + 2 * (items_i["origin"] - yy * g.rowp)
+    d_items_i = torch.from_numpy(items_i.view(np.uint8)).to(dev)
+    args_i = Args(tab_i.data_ptr(), gi, d_items_i.data_ptr(), d_n.data_ptr(), cap, d_w.data_ptr(),
+                  d_b.data_ptr(), d_r.data_ptr(), d_s.data_ptr(), K, 24, d_out.data_ptr(), d_t.data_ptr(), a.omask,
+                  a.fold)
     stream = torch.cuda.current_stream().cuda_stream
     ref = None
     res = {}
     for spec in a.variants.split(","):
         v, wv = (int(x) for x in spec.split(":"))
         d_out.zero_()
-        assert L.ib_run(v, wv, ctypes.byref(args), stream) == 0
+        av = args_i if v in (4, 9) else args
+        assert L.ib_run(v, wv, ctypes.byref(av), stream) == 0
         torch.cuda.synchronize()
         o = d_out.cpu().numpy().copy()
         if ref is None:
             ref = o
-        same = np.array_equal(o.view(np.uint32), ref.view(np.uint32)) if v != 2 else None
+        same = np.array_equal(o.view(np.uint32), ref.view(np.uint32)) if v in (0, 1, 3, 4, 8, 9, 10, 11) else None
         ts = []
         for _ in range(a.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            L.ib_run(v, wv, ctypes.byref(args), stream)
+            L.ib_run(v, wv, ctypes.byref(av), stream)
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))

@@ -113,59 +113,26 @@ __device__ __forceinline__ void patch_features2(const TabView &T, const P &pj, i
             }
 }
 
-// The same CalcFeature split in two phases for the software-pipelined item
-// loop: corner loads into a fixed 20-entry array (2 halves x up to 10
-// corners, index h*10 + r*(GW+1) + c), then the box sums from it.
-template <int GW, int GH, class P>
-__device__ __forceinline__ void patch_load(const TabView &T, const P &pj, int half_off, float4 (&cn)[20]) {
-    int col[GW + 1];
-#pragma unroll
-    for (int c = 0; c <= GW; c++) col[c] = pj.colq(c);
-#pragma unroll
-    for (int h = 0; h < 2; h++)
-#pragma unroll
-        for (int r = 0; r <= GH; r++) {
-            const int ro = h * half_off + pj.row0 + r * pj.rowstep;
-#pragma unroll
-            for (int c = 0; c <= GW; c++) cn[h * 10 + r * (GW + 1) + c] = T.at(ro + col[c]);
-        }
-}
-
-template <int GW, int GH>
-__device__ __forceinline__ void patch_box(const float4 (&cn)[20], f2 (&fp)[16]) {
-#pragma unroll
-    for (int h = 0; h < 2; h++)
-#pragma unroll
-        for (int r = 0; r < GH; r++)
-#pragma unroll
-            for (int c = 0; c < GW; c++) {
-                // (TL + BR) - (TR + BL), :385-412
-                const float4 tl = cn[h * 10 + r * (GW + 1) + c];
-                const float4 br = cn[h * 10 + (r + 1) * (GW + 1) + c + 1];
-                const float4 tr = cn[h * 10 + r * (GW + 1) + c + 1];
-                const float4 bl = cn[h * 10 + (r + 1) * (GW + 1) + c];
-                const int o = 4 * (r * GW + c) + 2 * h;
-                fp[o] = (f2{tl.x, tl.y} + f2{br.x, br.y}) - (f2{tr.x, tr.y} + f2{bl.x, bl.y});
-                fp[o + 1] = (f2{tl.z, tl.w} + f2{br.z, br.w}) - (f2{tr.z, tr.w} + f2{bl.z, bl.w});
-            }
-}
-
-#ifndef SC_ULOAD  // corners_load: one straight-line set of 20 loads for every shape
-#define SC_ULOAD 0
+#ifndef SC_SHAPE_LOADS  // 1: per-shape load branches (A/B only; the default is uniform loads)
+#define SC_SHAPE_LOADS 0
 #endif
+
+// Uniform corner set: every shape's corners as 10 slots per half, so one
+// straight-line sequence of loads serves a wave whatever shapes its lanes
+// hold.  Slot m is corner (r, c) = 2x2: (m/3, m%3) (slot 9 repeats (2,2), a
+// 2x2 patch has 9 corners); 1x4 (tall): (m/2, m%2); 4x1 (wide): (m/5, m%5).
+// Why: the texture addresser costs about the same per vector-memory
+// instruction however few lanes are active, and shape-divergent load
+// branches issued 2.1x the instructions of one uniform set (measured,
+// profiles/r2/itembench.md: item loop -11 %).
 template <class P>
-__device__ __forceinline__ void corners_load(const TabView &T, int half_off, const P &pj, float4 (&cn)[20]) {
-#if SC_ULOAD
-    // slot m of a half holds corner (r, c): 2x2 m = 3r + c (slot 9 repeats
-    // (2, 2)), 1x4 m = 2r + c, 4x1 m = 5r + c; the shapes differ only in the
-    // per-lane offsets, so the loads issue without divergence
+__device__ __forceinline__ void corner_offsets(const P &pj, int (&off)[10]) {
     int col[5], ro[5];
 #pragma unroll
     for (int c = 0; c < 5; c++) col[c] = pj.colq(c);
 #pragma unroll
     for (int r = 0; r < 5; r++) ro[r] = pj.row0 + r * pj.rowstep;
     const bool sq = pj.shape == 0, tall = pj.shape == 1;
-    int off[10];
 #pragma unroll
     for (int m = 0; m < 10; m++) {
         const int o0 = ro[m < 9 ? m / 3 : 2] + col[m < 9 ? m % 3 : 2];
@@ -173,25 +140,57 @@ __device__ __forceinline__ void corners_load(const TabView &T, int half_off, con
         const int o2 = ro[m / 5] + col[m % 5];
         off[m] = sq ? o0 : (tall ? o1 : o2);
     }
-#pragma unroll
-    for (int h = 0; h < 2; h++)
-#pragma unroll
-        for (int m = 0; m < 9; m++) cn[h * 10 + m] = T.at(h * half_off + off[m]);
-    if (!sq) {  // the strips' tenth corners (a 2x2 patch has 9)
-        cn[9] = T.at(off[9]);
-        cn[19] = T.at(half_off + off[9]);
-    }
-#else
-    if (pj.shape == 0) patch_load<2, 2>(T, pj, half_off, cn);
-    else if (pj.shape == 1) patch_load<1, 4>(T, pj, half_off, cn);
-    else patch_load<4, 1>(T, pj, half_off, cn);
-#endif
 }
 
-__device__ __forceinline__ void corners_box(int shape, const float4 (&cn)[20], f2 (&fp)[16]) {
-    if (shape == 0) patch_box<2, 2>(cn, fp);
-    else if (shape == 1) patch_box<1, 4>(cn, fp);
-    else patch_box<4, 1>(cn, fp);
+// Box sums of one half (4 channels) of the 4 cells from its 10 corner
+// slots: fh[2*cell], fh[2*cell+1] = channels (0,1), (2,3) of the half.
+template <int GW, int GH>
+__device__ __forceinline__ void half_box(const float4 (&cn)[10], f2 (&fh)[8]) {
+#pragma unroll
+    for (int r = 0; r < GH; r++)
+#pragma unroll
+        for (int c = 0; c < GW; c++) {
+            // (TL + BR) - (TR + BL), :385-412
+            const float4 tl = cn[r * (GW + 1) + c], br = cn[(r + 1) * (GW + 1) + c + 1];
+            const float4 tr = cn[r * (GW + 1) + c + 1], bl = cn[(r + 1) * (GW + 1) + c];
+            const int o = 2 * (r * GW + c);
+            fh[o] = (f2{tl.x, tl.y} + f2{br.x, br.y}) - (f2{tr.x, tr.y} + f2{bl.x, bl.y});
+            fh[o + 1] = (f2{tl.z, tl.w} + f2{br.z, br.w}) - (f2{tr.z, tr.w} + f2{bl.z, bl.w});
+        }
+}
+
+__device__ __forceinline__ void half_box(int shape, const float4 (&cn)[10], f2 (&fh)[8]) {
+    if (shape == 0) half_box<2, 2>(cn, fh);
+    else if (shape == 1) half_box<1, 4>(cn, fh);
+    else half_box<4, 1>(cn, fh);
+}
+
+// CalcFeature (:379-415) with uniform loads, one half at a time: the 10
+// loads of channels 0-3, their box sums, then the 10 loads of channels 4-7
+// (40 corner registers live instead of 80; measured as fast as all 20 loads
+// in flight at 12 waves per CU).  fp in the 32-feature order f[8 cell + 4 h + ch].
+template <class P>
+__device__ __forceinline__ void features_uniform(const TabView &T, int half_off, const P &pj, f2 (&fp)[16]) {
+    int off[10];
+    corner_offsets(pj, off);
+    f2 h[2][8];
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++) {
+        float4 cn[10];
+#pragma unroll
+        for (int m = 0; m < 10; m++) cn[m] = T.at(hh * half_off + off[m]);
+#if SC_LOAD_BARRIER
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+        half_box(pj.shape, cn, h[hh]);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        fp[4 * c] = h[0][2 * c];
+        fp[4 * c + 1] = h[0][2 * c + 1];
+        fp[4 * c + 2] = h[1][2 * c];
+        fp[4 * c + 3] = h[1][2 * c + 1];
+    }
 }
 
 // c_k = (q0+q1)+(q2+q3) of f[4k..4k+3] = fp[2k], fp[2k+1];
@@ -212,9 +211,13 @@ __device__ __forceinline__ void normalize2(f2 (&fp)[16]);
 // CalcFeature + Normalize (:379-457) of one projected patch.
 template <class P>
 __device__ __forceinline__ void descriptor2(const TabView &T, int half_off, const P &pj, f2 (&fp)[16]) {
+#if SC_SHAPE_LOADS
     if (pj.shape == 0) patch_features2<2, 2>(T, pj, half_off, fp);
     else if (pj.shape == 1) patch_features2<1, 4>(T, pj, half_off, fp);
     else patch_features2<4, 1>(T, pj, half_off, fp);
+#else
+    features_uniform(T, half_off, pj, fp);
+#endif
     normalize2(fp);
 }
 

@@ -54,10 +54,6 @@ namespace {
 #define SC_ABL_NOWAIT 0
 #endif
 
-#ifndef SC_PIPE  // item path: next item's corner loads in flight during this item's normalise + LR
-#define SC_PIPE 0
-#endif
-
 #ifndef SC_ITEM_BUF  // per-wave LDS results of the (survivor, weak) item path
 #define SC_ITEM_BUF 640
 #endif
@@ -320,51 +316,6 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
                     k = Ol[off + kk];
                 };
                 for (int b2 = 0; b2 < items; b2 += 64) stats.iter(min(64, items - b2));
-#if SC_PIPE
-                // software pipeline: once an item's box sums are taken, the
-                // corner loads of the lane's next item are issued, so they are
-                // in flight while this item normalises and runs its LR
-                float4 cn[20];
-                int kc = 0, ic = 0, shc = 0;
-                auto issue = [&](int t) {
-                    int k, i;
-                    decode(t, k, i);
-                    const int gk = off + k;
-                    const unsigned sv = surv[c + i];
-                    const TabView Tj{Tb, cell(sv) << 4};
-                    const auto pj = B.patch((int)(sv >> 16), (int)(sv & 0xffffu), gk);
-                    corners_load(Tj, half_off, pj, cn);
-                    kc = k;
-                    ic = i;
-                    shc = pj.shape;
-                };
-                if (lane < items) issue(lane);
-                for (int t2 = lane; t2 < items; t2 += 64) {
-                    f2 fp[16];
-                    corners_box(shc, cn, fp);
-                    const int k = kc, i = ic, gk = off + k;
-                    if (t2 + 64 < items) issue(t2 + 64);
-                    __builtin_amdgcn_sched_barrier(0);
-                    normalize2(fp);
-                    P[k * G + i] = LW ? lr_predict2(fp, Wl + gk * 9, Bl[gk]) : lr_predict2(fp, a.w + gk * 9, a.bias[gk]);
-                }
-#elif SC_ULOAD
-                for (int t2 = lane; t2 < items; t2 += 64) {
-                    int k, i;
-                    decode(t2, k, i);
-                    const int gk = off + k;
-                    const unsigned sv = surv[c + i];
-                    const TabView Tj{Tb, cell(sv) << 4};
-                    const auto pj = B.patch((int)(sv >> 16), (int)(sv & 0xffffu), gk);
-                    float4 cn[20];
-                    f2 fp[16];
-                    corners_load(Tj, half_off, pj, cn);
-                    __builtin_amdgcn_sched_barrier(0);
-                    corners_box(pj.shape, cn, fp);
-                    normalize2(fp);
-                    P[k * G + i] = LW ? lr_predict2(fp, Wl + gk * 9, Bl[gk]) : lr_predict2(fp, a.w + gk * 9, a.bias[gk]);
-                }
-#else
                 for (int t2 = lane; t2 < items; t2 += 64) {
                     int k, i;
                     decode(t2, k, i);
@@ -375,7 +326,6 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
                     P[k * G + i] = LW ? weak_eval(Tj, half_off, pj, Wl + gk * 9, Bl[gk])
                                       : weak_eval(Tj, half_off, pj, a.w + gk * 9, a.bias[gk]);
                 }
-#endif
                 wave_sync();
                 unsigned sv = 0;
                 float acc = 0.0f;  // GentleAdaboost.cpp:255-258 order
