@@ -166,6 +166,19 @@ int sc_mine(sc_detector *d, const uint8_t *gray, int w, int h, int stride_bytes,
  * 124-195, stays on the GPU for the trainer).  Windows still go to the host. */
 int sc_mine_device(sc_detector *d, const uint8_t *d_gray, int w, int h, int stride_bytes,
                    sc_window *wins, float *d_features, int capacity, int *n_out);
+/* FillNegSamples over n negative images of one size in one pass (the
+ * reference loops over its image list, DenseSURFFeatureExtractor.cpp:
+ * 132-190): candidates in (image, level, y, x) order, the first `capacity`
+ * of the whole batch kept, windows back to back; n_out[f] = image f's
+ * candidates (all of them, kept or not).  sc_mine is the n = 1 case.  The
+ * device form takes n frames at d_frames + f*h*stride and writes the
+ * descriptors to device memory, as sc_mine_device. */
+int sc_mine_batch(sc_detector *d, const uint8_t *const *frames, int n, int w, int h,
+                  int stride_bytes, sc_window *wins, float *features, int capacity,
+                  int *n_out);
+int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, int h,
+                         int stride_bytes, sc_window *wins, float *d_features, int capacity,
+                         int *n_out);
 
 /* ---- introspection / parity dumps -------------------------------------- */
 #define SC_INFO_LEVELS 1        /* levels used for the last geometry         */

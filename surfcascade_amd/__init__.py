@@ -56,7 +56,7 @@ EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_mode
            "sc_stream_wait_detector", "sc_detector_info",
            "sc_detector_set_shard", "sc_detector_set_option", "sc_detector_set_debug", "sc_debug_dump", "sc_set_timing", "sc_get_timing",
            "sc_group_rectangles", "sc_group_detections", "sc_fddb_format",
-           "sc_miner_create", "sc_mine", "sc_mine_device", "sc_fast_nms", "sc_decode_jpeg_gray", "sc_imread_gray",
+           "sc_miner_create", "sc_mine", "sc_mine_device", "sc_mine_batch", "sc_mine_batch_device", "sc_fast_nms", "sc_decode_jpeg_gray", "sc_imread_gray",
            "sc_last_error", "sc_version")
 
 
@@ -154,6 +154,8 @@ def load_library():
     L.sc_miner_create.argtypes = [vp, i32, i32, i32, P(vp)]
     L.sc_mine.argtypes = [vp, vp, i32, i32, i32, vp, vp, i32, P(i32)]
     L.sc_mine_device.argtypes = [vp, vp, i32, i32, i32, vp, vp, i32, P(i32)]
+    L.sc_mine_batch.argtypes = [vp, P(vp), i32, i32, i32, i32, vp, vp, i32, vp]
+    L.sc_mine_batch_device.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp, i32, vp]
     L.sc_group_rectangles.argtypes = [vp, i32, i32, ctypes.c_double, vp, i32, P(i32)]
     L.sc_group_detections.argtypes = [vp, i32, i32, i32, ctypes.c_double, vp, i32, vp, P(i32)]
     L.sc_fddb_format.argtypes = [ctypes.c_char_p, vp, i32, ctypes.c_char_p, sz, P(sz)]
@@ -582,6 +584,50 @@ class Miner(Detector):
             _check(rc)
         k = min(n.value, capacity)
         return wins[:k].copy(), (feat[:k].copy() if features else None), n.value
+
+    def mine_batch(self, imgs, capacity, features=True):
+        """FillNegSamples over a list of same-size negative images in one pass
+        -> (windows in (image, level, y, x) order, descriptors or None,
+        per-image candidate counts int32 [n]); the first `capacity` windows of
+        the batch are kept (an image's windows follow the previous image's)."""
+        imgs = [np.ascontiguousarray(im, np.uint8) for im in imgs]
+        H, W = imgs[0].shape
+        if any(im.shape != (H, W) for im in imgs):
+            raise ValueError("images of one size")
+        ptrs = (ctypes.c_void_p * len(imgs))(*[im.ctypes.data for im in imgs])
+        wins = np.zeros(max(capacity, 1), WINDOW_DTYPE)
+        feat = np.zeros((max(capacity, 1), self.n_patches, 32), np.float32) if features else None
+        counts = np.zeros(len(imgs), np.int32)
+        rc = load_library().sc_mine_batch(self._h, ptrs, len(imgs), W, H, W, wins.ctypes.data,
+                                          feat.ctypes.data if features else None, capacity,
+                                          counts.ctypes.data)
+        if rc != -6:
+            _check(rc)
+        k = min(int(counts.sum()), capacity)
+        return wins[:k].copy(), (feat[:k].copy() if features else None), counts
+
+    def mine_batch_device(self, frames, capacity, features=None):
+        """Device frames (uint8 [n, H, W] tensor, rows contiguous) -> (windows,
+        per-image counts); descriptors into `features` (device) when given."""
+        if frames.dim() != 3 or frames.element_size() != 1 or not frames.is_cuda or frames.stride(2) != 1 \
+                or frames.stride(0) != frames.shape[1] * frames.stride(1):
+            raise ValueError("frames must be a uint8 [n, H, W] device tensor, frames back to back")
+        n, H, W = frames.shape
+        if features is not None and (not features.is_cuda or features.element_size() != 4
+                                     or not features.is_contiguous()
+                                     or features.numel() < capacity * self.n_patches * 32):
+            raise ValueError("features must be a contiguous float32 device tensor of "
+                             "capacity * n_patches * 32 values")
+        self._after_torch(frames, features)
+        wins = np.zeros(max(capacity, 1), WINDOW_DTYPE)
+        counts = np.zeros(n, np.int32)
+        rc = load_library().sc_mine_batch_device(self._h, frames.data_ptr(), n, W, H, frames.stride(1),
+                                                 wins.ctypes.data,
+                                                 features.data_ptr() if features is not None else None,
+                                                 capacity, counts.ctypes.data)
+        if rc != -6:
+            _check(rc)
+        return wins[:min(int(counts.sum()), capacity)].copy(), counts
 
     def mine_device(self, frame, capacity, features=None):
         """Device frame (uint8 [H, W] tensor) -> (windows, total); the

@@ -139,6 +139,7 @@ struct sc_detector {
     DevBuf<sc::ProjPatch> d_proj_all;
     DevBuf<int> d_mine_cnt, d_mine_off;
     DevBuf<sc::MineWindow> d_mine_win;
+    DevBuf<int> d_mine_fc;  // [1 + n]: candidates of the batch, per frame
     DevBuf<float> d_feat;
     DevBuf<sc::TaskDesc> d_tasks;
     // working buffers
@@ -775,80 +776,86 @@ int detect_device_sync(sc_detector *d, const uint8_t *d_frames, int n, int W, in
     return SC_OK;
 }
 
-// FillNegSamples' scan of one device frame: the shared integral + cascade
-// kernels on the stride-10 grid, then candidate selection and descriptors.
-int mine_sync(sc_detector *d, const uint8_t *d_frame, int W, int H, int stride, sc_window *wins,
+// FillNegSamples' scan of n device frames of one size (frame f at
+// d_frames + f*H*stride): the shared integral + cascade kernels on the
+// stride-10 grid, then candidate selection -- block counts, a device scan,
+// the scatter -- and descriptors, with one host synchronisation at the end.
+// Candidates in (frame, level, y, x) order; the first `capacity` are kept;
+// n_out[f] = frame f's candidates (all of them).
+int mine_sync(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int stride, sc_window *wins,
               float *feat, int capacity, int *n_out, bool feat_device = false) {
     if (!d->miner) throw Error{SC_ERR_INVALID, "not a miner (sc_miner_create)"};
-    if (!d_frame || !n_out || capacity < 0 || (capacity > 0 && !wins))
+    if (!d_frames || !n_out || n <= 0 || capacity < 0 || (capacity > 0 && !wins))
         throw Error{SC_ERR_INVALID, "bad arguments"};
     if (stride < W) throw Error{SC_ERR_INVALID, "stride smaller than width"};
-    d->d_counters.ensure(2);
-    enqueue(d, d_frame, 1, W, H, stride, nullptr, 0, d->d_counters.p);
+    d->d_counters.ensure((size_t)n + 1);
+    enqueue(d, d_frames, n, W, H, stride, nullptr, 0, d->d_counters.p);
     const Geometry &g = d->geo;
-    *n_out = 0;
+    for (int f = 0; f < n; f++) n_out[f] = 0;
     if (g.grid == 0) {
         HIPCHK(hipStreamSynchronize(d->stream));
         return SC_OK;
     }
-    const int nb = (int)((g.grid + sc::kMineBlock - 1) / sc::kMineBlock);
+    const int bpf = (int)((g.grid + sc::kMineBlock - 1) / sc::kMineBlock);
+    if ((long long)bpf * n > INT32_MAX / 2) throw Error{SC_ERR_INVALID, "batch too large"};
+    const int nb = bpf * n;
     d->d_mine_cnt.ensure(nb);
     d->d_mine_off.ensure(nb);
+    d->d_mine_fc.ensure((size_t)n + 1);
     d->d_mine_win.ensure(std::max(capacity, 1));
     sc::MineArgs ma{};
     ma.st_p = d->d_st_p.p;
     ma.st_s = d->d_st_s.p;
     ma.grid = g.grid;
+    ma.n_frames = n;
+    ma.bpf = bpf;
     ma.n_stages = d->S;
     ma.step = g.step;
     ma.n_levels = g.n_levels;
     ma.levels = d->d_levels.p;
     ma.block_count = d->d_mine_cnt.p;
     ma.block_offset = d->d_mine_off.p;
+    ma.frame_count = d->d_mine_fc.p;
     ma.out = d->d_mine_win.p;
     ma.capacity = capacity;
     sc::launch_mine_count(ma, d->stream);
     HIPCHK(hipGetLastError());
-    std::vector<int> cnt(nb);
-    HIPCHK(hipMemcpyAsync(cnt.data(), d->d_mine_cnt.p, sizeof(int) * nb, hipMemcpyDeviceToHost,
-                          d->stream));
-    HIPCHK(hipStreamSynchronize(d->stream));
-    long long total = 0;
-    for (int b = 0; b < nb; b++) {
-        const int c = cnt[b];
-        cnt[b] = (int)std::min<long long>(total, INT32_MAX);
-        total += c;
-    }
-    HIPCHK(hipMemcpyAsync(d->d_mine_off.p, cnt.data(), sizeof(int) * nb, hipMemcpyHostToDevice,
-                          d->stream));
+    sc::launch_mine_scan(ma, d->stream);
+    HIPCHK(hipGetLastError());
     sc::launch_mine_scatter(ma, d->stream);
     HIPCHK(hipGetLastError());
-    const int kept = (int)std::min<long long>(total, capacity);
+    // descriptors of every kept window: kept = min(total, capacity) is only
+    // known on the device, so the feature kernel covers `capacity` windows
+    // and its threads past the total exit (they read the scan's total)
     const int P = (int)d->all_rects.size() / 4;
-    if (feat && kept > 0) {
-        if (!feat_device) d->d_feat.ensure((size_t)kept * P * 32);
+    if (feat && capacity > 0) {
+        if (!feat_device) d->d_feat.ensure((size_t)capacity * P * 32);
         sc::FeatureArgs fa{};
         fa.table = d->d_table.p;
         fa.g = g.tg;
         fa.windows = d->d_mine_win.p;
-        fa.n_windows = kept;
+        fa.n_windows = capacity;
+        fa.n_valid = d->d_mine_fc.p;
         fa.n_patches = P;
         fa.proj_all = d->d_proj_all.p;
         fa.out = feat_device ? feat : d->d_feat.p;
         sc::launch_features(fa, d->stream);
         HIPCHK(hipGetLastError());
-        if (!feat_device)
-            HIPCHK(hipMemcpyAsync(feat, d->d_feat.p, sizeof(float) * (size_t)kept * P * 32,
-                                  hipMemcpyDeviceToHost, d->stream));
     }
+    std::vector<int> fc((size_t)n + 1);
+    HIPCHK(hipMemcpyAsync(fc.data(), d->d_mine_fc.p, sizeof(int) * (n + 1), hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    long long total = 0;
+    for (int f = 0; f < n; f++) total += fc[1 + f];
+    const int kept = (int)std::min<long long>(total, capacity);
+    if (feat && kept > 0 && !feat_device)
+        HIPCHK(hipMemcpy(feat, d->d_feat.p, sizeof(float) * (size_t)kept * P * 32, hipMemcpyDeviceToHost));
     std::vector<sc::MineWindow> mw(kept);
     if (kept > 0)
-        HIPCHK(hipMemcpyAsync(mw.data(), d->d_mine_win.p, sizeof(sc::MineWindow) * kept,
-                              hipMemcpyDeviceToHost, d->stream));
-    HIPCHK(hipStreamSynchronize(d->stream));
+        HIPCHK(hipMemcpy(mw.data(), d->d_mine_win.p, sizeof(sc::MineWindow) * kept, hipMemcpyDeviceToHost));
     for (int i = 0; i < kept; i++)
         wins[i] = sc_window{mw[i].level, mw[i].x, mw[i].y, mw[i].l, mw[i].l, d->S, (double)mw[i].score};
-    *n_out = (int)std::min<long long>(total, INT32_MAX);
+    for (int f = 0; f < n; f++) n_out[f] = fc[1 + f];
     if (total > capacity) {
         g_err = "capacity " + std::to_string(capacity) + " < " + std::to_string(total) +
                 " candidates (the first " + std::to_string(capacity) + " were returned)";
@@ -1163,28 +1170,38 @@ int sc_miner_create(const sc_model *m, int tmpl_w, int tmpl_h, int device, sc_de
     });
 }
 
-int sc_mine(sc_detector *d, const uint8_t *gray, int w, int h, int stride, sc_window *wins,
-            float *features, int capacity, int *n_out) {
+int sc_mine_batch(sc_detector *d, const uint8_t *const *frames, int n, int w, int h, int stride,
+                  sc_window *wins, float *features, int capacity, int *n_out) {
     return guarded([&] {
-        if (!d || !gray) throw Error{SC_ERR_INVALID, "bad arguments"};
+        if (!d || !frames || n <= 0) throw Error{SC_ERR_INVALID, "bad arguments"};
         if (w < 2 || h < 2 || stride < w) throw Error{SC_ERR_INVALID, "bad frame geometry"};
         HIPCHK(hipSetDevice(d->device));
-        const uint8_t *fr[1] = {gray};
-        upload_frames(d, fr, 1, w, h, stride);
-        return mine_sync(d, d->d_frames.p, w, h, w, wins, features, capacity, n_out);
+        upload_frames(d, frames, n, w, h, stride);
+        return mine_sync(d, d->d_frames.p, n, w, h, w, wins, features, capacity, n_out);
     });
+}
+
+int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, int h, int stride,
+                         sc_window *wins, float *d_features, int capacity, int *n_out) {
+    return guarded([&] {
+        if (!d || !d_frames || n <= 0) throw Error{SC_ERR_INVALID, "bad arguments"};
+        if (w < 2 || h < 2 || stride < w) throw Error{SC_ERR_INVALID, "bad frame geometry"};
+        HIPCHK(hipSetDevice(d->device));
+        check_device_ptr(d, d_frames, "d_frames");
+        check_device_ptr(d, d_features, "d_features");
+        return mine_sync(d, d_frames, n, w, h, stride, wins, d_features, capacity, n_out, true);
+    });
+}
+
+int sc_mine(sc_detector *d, const uint8_t *gray, int w, int h, int stride, sc_window *wins,
+            float *features, int capacity, int *n_out) {
+    const uint8_t *fr[1] = {gray};
+    return sc_mine_batch(d, fr, 1, w, h, stride, wins, features, capacity, n_out);
 }
 
 int sc_mine_device(sc_detector *d, const uint8_t *d_gray, int w, int h, int stride, sc_window *wins,
                    float *d_features, int capacity, int *n_out) {
-    return guarded([&] {
-        if (!d || !d_gray) throw Error{SC_ERR_INVALID, "bad arguments"};
-        if (w < 2 || h < 2 || stride < w) throw Error{SC_ERR_INVALID, "bad frame geometry"};
-        HIPCHK(hipSetDevice(d->device));
-        check_device_ptr(d, d_gray, "d_gray");
-        check_device_ptr(d, d_features, "d_features");
-        return mine_sync(d, d_gray, w, h, stride, wins, d_features, capacity, n_out, true);
-    });
+    return sc_mine_batch_device(d, d_gray, 1, w, h, stride, wins, d_features, capacity, n_out);
 }
 
 int sc_detect_batch(sc_detector *d, const uint8_t *const *frames, int n, int w, int h, int stride,

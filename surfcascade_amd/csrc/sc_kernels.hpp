@@ -177,32 +177,39 @@ struct WalkArgs {
 constexpr int kMineBlock = 1024;  // grid windows per selection block
 
 struct MineWindow {
-    int level, x, y, l;
+    int frame, level, x, y, l;
     float score;  // last stage score
 };
 
+// A batch of n_frames images of one size: per-window results [frame][grid];
+// selection blocks of kMineBlock windows never straddle two frames (bpf
+// blocks per frame), so block counts also give per-frame counts.
 struct MineArgs {
     const int8_t *st_p;
     const float *st_s;
-    long long grid;
+    long long grid;           // windows per frame
+    int n_frames, bpf;
     int n_stages, step, n_levels;
     const LevelInfo *levels;
-    int *block_count;         // [blocks] candidates per block
-    const int *block_offset;  // [blocks] exclusive prefix
+    int *block_count;         // [n_frames * bpf] candidates per block
+    int *block_offset;        // [n_frames * bpf] exclusive prefix (device scan), saturated at INT32_MAX
+    int *frame_count;         // [1 + n_frames]: [0] all candidates (saturated), [1+f] frame f's
     MineWindow *out;
     int capacity;
 };
 
 struct FeatureArgs {
-    const float4 *table;  // frame 0's table
+    const float4 *table;  // frame 0's table (frame f's at + f * g.frame4)
     TableGeom g;
     const MineWindow *windows;
     int n_windows, n_patches;
+    const int *n_valid;  // when set, *n_valid (saturated total) bounds the windows described
     const ProjPatch *proj_all;  // [n_levels][2 parities][n_patches]: every template patch
     float *out;                 // [n_windows][n_patches][32]
 };
 
 void launch_mine_count(const MineArgs &a, hipStream_t s);
+void launch_mine_scan(const MineArgs &a, hipStream_t s);
 void launch_mine_scatter(const MineArgs &a, hipStream_t s);
 void launch_features(const FeatureArgs &a, hipStream_t s);
 

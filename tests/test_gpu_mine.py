@@ -93,3 +93,57 @@ def test_mine_device_descriptors_stay_on_gpu(sc, oracle):
     f = feats.view(cap, m.n_patches, 32)[:len(wins)].cpu().numpy()
     assert np.array_equal(f.view(np.uint32), hf.view(np.uint32))
     _check((wins, f, n), oracle.mine(oracle.integral(img), oracle.empty_cascade(), cap))
+
+
+def _oracle_batch(oracle, imgs, casc, cap):
+    """Per-image oracle scans concatenated in image order, the first `cap` kept."""
+    ws, fs, counts = [], [], []
+    for im in imgs:
+        T = oracle.integral(im)
+        _, _, n = oracle.mine(T, casc, 1 << 16, features=False)
+        w, f, n = oracle.mine(T, casc, max(n, 1))
+        w, f = w[:n], f[:n]
+        ws.append(w)
+        fs.append(f)
+        counts.append(n)
+    w = np.concatenate(ws)[:cap]
+    f = np.concatenate(fs)[:cap]
+    return w, f, counts
+
+
+def test_mine_batch_matches_per_image_oracle(sc, oracle, face_cascade):
+    # sc_mine_batch: FillNegSamples over an image list in one pass (the
+    # reference's loop over negatives, DenseSURFFeatureExtractor.cpp:132-190);
+    # the capacity cut falls inside the third image
+    from surfcascade_amd import synth
+    c = face_cascade
+    theta = np.full(c.n_stages, 0.42, np.float32)
+    text = synth.write_cfg(synth.cascade_tree(c.n_weak, theta, c.patch_index, c.w, c.bias))
+    casc_or = oracle.cascade_from_cfg(text)
+    imgs = [_frame(240, 200, 60 + k) for k in range(5)]
+    rw, rf, rc = _oracle_batch(oracle, imgs, casc_or, 1 << 20)
+    assert min(rc) > 0
+    m = sc.Miner(sc.Model.parse(text))
+    cap = rc[0] + rc[1] + rc[2] // 2
+    gw, gf, gc = m.mine_batch(imgs, cap)
+    assert list(gc) == rc
+    _check((gw, gf, sum(rc)), (rw[:cap], rf[:cap], sum(rc)))
+    # everything kept, and the single-image entry point is the n = 1 batch
+    gw, gf, gc = m.mine_batch(imgs, sum(rc), features=False)
+    assert _win(gw) == _win(rw)
+    w1, f1, n1 = m.mine(imgs[3], 1 << 12)
+    assert n1 == rc[3] and _win(w1) == _win(rw[sum(rc[:3]):sum(rc[:4])])
+
+
+def test_mine_batch_device_first_round(sc, oracle):
+    import torch
+    imgs = [_frame(200, 160, 70 + k) for k in range(3)]
+    m = sc.Miner(None)
+    cap = 700  # first round: every window; the cut falls in the second image
+    feats = torch.zeros(cap * m.n_patches * 32, dtype=torch.float32, device="cuda:0")
+    d = torch.from_numpy(np.stack(imgs)).to("cuda:0")
+    wins, counts = m.mine_batch_device(d, cap, feats)
+    rw, rf, rc = _oracle_batch(oracle, imgs, oracle.empty_cascade(), cap)
+    assert list(counts) == rc and sum(rc) > cap
+    f = feats.view(cap, m.n_patches, 32)[:len(wins)].cpu().numpy()
+    _check((wins, f, sum(rc)), (rw, rf, sum(rc)))
