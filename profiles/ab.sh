@@ -9,6 +9,6 @@ mkdir -p "$R/$OUT"
 for r in $(seq 1 "$ROUNDS"); do
   for v in "${V[@]}"; do
     SURFCASCADE_LIB="$R/surfcascade_amd/lib/variants/$v/libsurfcascade.so" timeout -k 10 200 \
-      python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu --latency-steps 0 --host-steps 0 "$@" > "$R/$OUT/$v.$r.json" 2>/dev/null || exit 1
+      python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu --latency-steps 0 --host-steps 0 "$@" > "$R/$OUT/$v.$r.json" 2> "$R/$OUT/$v.$r.err" || { tail -5 "$R/$OUT/$v.$r.err"; exit 1; }
   done
 done

@@ -577,6 +577,83 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_uhalf(Args a) {
     }
 }
 
+// V12: one item per lane on the interleaved 32-B-cell table (TableGeom cs 2),
+// loads paired across the wave's halves: for each corner slot, instruction X
+// reads cell(A).h0 in lane i < 32 and cell(A).h1 in lane i + 32 (A = lane
+// i's item), instruction Y reads cell(B).h0 in lane i and cell(B).h1 in lane
+// i + 32 (B = lane i + 32's item): each instruction's lane pair touches one
+// 32-B cell, i.e. one cache line, instead of the channel-split layout's two
+// lines per lane in sparse stages (dense stages: the same 8 lines per 1 KiB).
+// One v_permlane32_swap per dword then gives every lane both halves of its
+// own item (X' = own h0, Y' = own h1).  All 20 loads in flight.
+template <int SW>
+__device__ __forceinline__ auto swp(unsigned a, unsigned b) {
+    if constexpr (SW == 32) return __builtin_amdgcn_permlane32_swap(a, b, false, false);
+    else return __builtin_amdgcn_permlane16_swap(a, b, false, false);
+}
+
+// V13: V12 with the pairs (i, i + 16) of v_permlane16_swap (rows 0/1, 2/3)
+template <int WAVES, int SW>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_xswap(Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4 *Wl; double *Bl; int4 *Rl; float *Sc;
+    stage<WAVES>(a, smem, Wl, Bl, Rl, Sc);
+    const int lane = threadIdx.x & 63;
+    const unsigned hoff = (lane & SW) ? 16u : 0u;  // SW 32: pairs (i, i+32); 16: (i, i+16)
+    const unsigned q0 = xcc();
+    const char *Tb = reinterpret_cast<const char *>(a.table);
+    for (unsigned qi = 0; qi < 8; qi++) {
+      const unsigned q = (q0 + qi) & 7;
+      const Item *I = a.items + q * a.cap;
+      float *O = a.out + q * a.cap;
+      const int n = a.n_items[q];
+      for (;;) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&a.tickets[q * 64], 1);
+        b0 = __builtin_amdgcn_readfirstlane(b0) * kChunk * kBlock;
+        if (b0 >= n) break;
+        const int b1 = min(n, b0 + kChunk * kBlock);
+        for (int c = b0; c < b1; c += 64) {
+            const int i = c + lane;
+            const Item it = I[i < b1 ? i : b0];
+            const InlinePatch pj = project(a, Rl, Sc, it);
+            int off[10];
+            corner_offsets(pj, off);
+            float4 X[10], Y[10];
+#pragma unroll
+            for (int m = 0; m < 10; m++) {
+                const unsigned own = (it.origin + (unsigned)off[m]) << 4;
+                const auto pa = swp<SW>(own, own);
+                X[m] = *reinterpret_cast<const float4 *>(Tb + (pa[0] + hoff));
+                Y[m] = *reinterpret_cast<const float4 *>(Tb + (pa[1] + hoff));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            float4 c0[10], c1[10];
+#pragma unroll
+            for (int m = 0; m < 10; m++) {
+                const auto sx = swp<SW>(__float_as_uint(X[m].x), __float_as_uint(Y[m].x)); 
+                const auto sy = swp<SW>(__float_as_uint(X[m].y), __float_as_uint(Y[m].y));
+                const auto sz = swp<SW>(__float_as_uint(X[m].z), __float_as_uint(Y[m].z));
+                const auto sw = swp<SW>(__float_as_uint(X[m].w), __float_as_uint(Y[m].w));
+                c0[m] = make_float4(__uint_as_float(sx[0]), __uint_as_float(sy[0]), __uint_as_float(sz[0]), __uint_as_float(sw[0]));
+                c1[m] = make_float4(__uint_as_float(sx[1]), __uint_as_float(sy[1]), __uint_as_float(sz[1]), __uint_as_float(sw[1]));
+            }
+            f2 h0[8], h1[8], fp[16];
+            half_box(pj.shape, c0, h0);
+            half_box(pj.shape, c1, h1);
+#pragma unroll
+            for (int cl = 0; cl < 4; cl++) {
+                fp[4 * cl] = h0[2 * cl]; fp[4 * cl + 1] = h0[2 * cl + 1];
+                fp[4 * cl + 2] = h1[2 * cl]; fp[4 * cl + 3] = h1[2 * cl + 1];
+            }
+            normalize2(fp);
+            const float p = lr_predict2(fp, Wl + it.k * 9, Bl[it.k]);
+            if (i < b1) O[i] = p;
+        }
+      }
+    }
+}
+
 // A3 (ablation, wrong results): the production item with every corner's
 // table row folded into a band of (fold+1) rows (row & fold): the same
 // lanes->lines pattern per wave-instruction, a table footprint the XCD's L2
@@ -686,6 +763,14 @@ extern "C" int ib_run(int variant, int waves, const Args *a, void *stream) {
         if (variant == 5) hipLaunchKernelGGL((k_abl<12, 1>), dim3(cus), dim3(768), lds, s, *a);
         else if (variant == 6) hipLaunchKernelGGL((k_abl<12, 2>), dim3(cus), dim3(768), lds, s, *a);
         else hipLaunchKernelGGL((k_abl<12, 3>), dim3(cus), dim3(768), lds, s, *a);
+    } else if (variant == 12) {
+        if (waves == 12) hipLaunchKernelGGL((k_xswap<12, 32>), dim3(cus), dim3(768), lds, s, *a);
+        else if (waves == 16) hipLaunchKernelGGL((k_xswap<16, 32>), dim3(cus), dim3(1024), lds, s, *a);
+        else return -1;
+    } else if (variant == 13) {
+        if (waves == 12) hipLaunchKernelGGL((k_xswap<12, 16>), dim3(cus), dim3(768), lds, s, *a);
+        else if (waves == 16) hipLaunchKernelGGL((k_xswap<16, 16>), dim3(cus), dim3(1024), lds, s, *a);
+        else return -1;
     } else if (variant == 3) {
         if (waves == 8) L(k_fold, 8); else if (waves == 12) L(k_fold, 12); else if (waves == 16) L(k_fold, 16); else return -1;
     } else {

@@ -208,13 +208,13 @@ def main():
     for spec in a.variants.split(","):
         v, wv = (int(x) for x in spec.split(":"))
         d_out.zero_()
-        av = args_i if v in (4, 9) else args
+        av = args_i if v in (4, 9, 12, 13) else args
         assert L.ib_run(v, wv, ctypes.byref(av), stream) == 0
         torch.cuda.synchronize()
         o = d_out.cpu().numpy().copy()
         if ref is None:
             ref = o
-        same = np.array_equal(o.view(np.uint32), ref.view(np.uint32)) if v in (0, 1, 3, 4, 8, 9, 10, 11) else None
+        same = np.array_equal(o.view(np.uint32), ref.view(np.uint32)) if v in (0, 1, 3, 4, 8, 9, 10, 11, 12, 13) else None
         ts = []
         for _ in range(a.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
