@@ -20,13 +20,22 @@ KERNELS = {"window_kernel": "windows", "cascade_kernel": "windows", "chain_kerne
 
 
 def load(d):
+    """Per kernel and counter, the mean over the batch's launches.  A pass may
+    also hold launches of another shape (a batch-1 leg, a chunk tail): only
+    dispatches lasting at least half the kernel's longest in that pass count."""
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(d, "*", "pmc_counter_collection.csv")):
+        rows = []
         for row in csv.DictReader(open(f)):
             name = next((v for k, v in KERNELS.items() if k in row["Kernel_Name"]), None)
-            if name is None:
-                continue
-            acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            if name is not None:
+                rows.append((name, int(row["End_Timestamp"]) - int(row["Start_Timestamp"]), row))
+        longest = collections.defaultdict(int)
+        for name, dur, _ in rows:
+            longest[name] = max(longest[name], dur)
+        for name, dur, row in rows:
+            if dur * 2 >= longest[name]:
+                acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 

@@ -717,7 +717,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
                     nseg[sl] = min(nx, j0[sl] + nxs) - j0[sl];
                     nvis[sl] = 0;
                     st[sl] = 1;
-                    if (qq == 0) start(sl, 0);
+                    if (qq == 0 || SC_ABL_NOWAIT) start(sl, j0[sl]);  // (segment 0 enters at 0)
                 }
                 SC_PROF(c_deq);
             }
