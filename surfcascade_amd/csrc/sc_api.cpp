@@ -620,7 +620,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     ca.st_p = d->d_st_p.p;
     ca.st_s = d->d_st_s.p;
     HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kQueueWords, d->stream));
-    const int seg_max = (g.nx_max + sc::kXcds - 1) / sc::kXcds;  // chain kernel segments
+    const int seg_max = (g.nx_max + sc::kChainSegs - 1) / sc::kChainSegs;  // chain kernel segments
     const bool lazy = d->lazy && sc::chain_lds_bytes(d->K, seg_max, g.n_levels) <= 160 * 1024;
     if (!lazy) {
         timed_begin(d, &e0);

@@ -27,6 +27,13 @@ constexpr int kXcds = 8;          // MI355X: 8 XCDs, one L2 each
 constexpr int kQueueStride = 64;  // ints between per-XCD queue words (own 256-B line each)
 constexpr int kMaxSubQ = 8;       // chain kernel: dequeue counters per XCD queue, at most
 constexpr int kQueueWords = kXcds * kMaxSubQ * kQueueStride;  // the queue buffer
+#ifndef SC_NSEG
+#define SC_NSEG 8
+#endif
+// chain kernel: segments per row; XCD x serves segment x / (kXcds / kChainSegs)
+// and, of that segment, the rows of class x % (kXcds / kChainSegs)
+constexpr int kChainSegs = SC_NSEG;
+static_assert(kChainSegs >= 1 && kXcds % kChainSegs == 0, "segments per row divide the XCD count");
 
 struct TableGeom {
     int W, H, step;
