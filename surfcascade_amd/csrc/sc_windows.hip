@@ -369,7 +369,7 @@ __device__ __forceinline__ void stage_model(const CascadeArgs &a, unsigned char 
 template <bool LW>
 __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_kernel(CascadeArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: per-wave LDS bases in SGPRs)
     float4 *Wl;
     double *Bl;
     int16_t *Ol;
@@ -604,7 +604,7 @@ template <bool LW>
 __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(CascadeArgs a,
                                                                                   WalkArgs w) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: per-wave LDS bases in SGPRs)
     float4 *Wl;
     double *Bl;
     int16_t *Ol;
