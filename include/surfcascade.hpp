@@ -275,6 +275,31 @@ class Miner {
         }
         return features_all.size() >= n_total;
     }
+    // The same over several negative images of one size in one pass
+    // (sc_mine_batch): the loop of :132-190 over a chunk of the image list.
+    bool FillNegSamples(const std::vector<const uint8_t *> &grays, int w, int h, int stride,
+                        std::vector<std::vector<std::vector<float>>> &features_all, size_t n_total) {
+        if (features_all.size() >= n_total || grays.empty()) return features_all.size() >= n_total;
+        const int want = (int)(n_total - features_all.size());
+        std::vector<sc_window> wins(want);
+        std::vector<float> feat((size_t)want * n_patches_ * 32);
+        std::vector<int> counts(grays.size());
+        const int rc = sc_mine_batch(det_.get(), grays.data(), (int)grays.size(), w, h, stride, wins.data(),
+                                     feat.data(), want, counts.data());
+        if (rc != SC_ERR_CAPACITY) check(rc);
+        long long total = 0;
+        for (int c : counts) total += c;
+        const int kept = (int)std::min<long long>(total, want);
+        for (int i = 0; i < kept; i++) {
+            std::vector<std::vector<float>> sample(n_patches_);
+            for (int j = 0; j < n_patches_; j++) {
+                const float *f = &feat[((size_t)i * n_patches_ + j) * 32];
+                sample[j].assign(f, f + 32);
+            }
+            features_all.push_back(std::move(sample));
+        }
+        return features_all.size() >= n_total;
+    }
 
    private:
     struct Free {

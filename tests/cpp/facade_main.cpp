@@ -57,6 +57,11 @@ int main(int argc, char **argv) {
         std::vector<std::vector<std::vector<float>>> negs;
         const bool full = miner.FillNegSamples(img.data(), w, h, w, negs, 5);
         std::printf("mined %zu %d %.9g\n", negs.size(), (int)full, negs.empty() ? 0.0 : negs[4][607][31]);
+        // the batch form over [img, img]: the first 5 samples are img's again
+        std::vector<std::vector<std::vector<float>>> negs2;
+        const std::vector<const uint8_t *> batch = {img.data(), img.data()};
+        const bool full2 = miner.FillNegSamples(batch, w, h, w, negs2, 5);
+        std::printf("minedb %zu %d %.9g\n", negs2.size(), (int)full2, negs2.empty() ? 0.0 : negs2[4][607][31]);
     }
     return 0;
 }

@@ -54,11 +54,12 @@ def test_facade_detect_matches_oracle(facade_bin, tmp_path, oracle):
     assert got == exp
     # then groupRectangles + the FDDB block (ObjDetector.cpp:223-231)
     import surfcascade_amd as sc
-    mined = lines[-1].split()
+    mined, minedb = lines[-2].split(), lines[-1].split()
     assert mined[:3] == ["mined", "5", "1"]
+    assert minedb[:3] == ["minedb", "5", "1"] and minedb[3] == mined[3]
     _, feat, _ = oracle.mine(oracle.integral(img), oracle.empty_cascade(), 5)
     assert np.float32(float(mined[3])) == feat[4, 607, 31]
-    lines = lines[:-1]
+    lines = lines[:-2]
     block = "\n".join(lines[k + 1 + nd:]) + "\n"
     assert block == oracle.fddb_format("frame", oracle.group_rectangles(sc._as_rects(ref)))
 
