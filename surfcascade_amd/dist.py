@@ -76,7 +76,10 @@ def _gather_records(gm, counts, recs, group):
     nb = max(ns) * RECORD_DTYPE.itemsize  # every rank sends its first max(count) records
     gr = [torch.zeros(nb, dtype=recs.dtype, device=recs.device) for _ in gm]
     if nb > 0:
-        dist.all_gather(gr, recs[:nb].contiguous(), group=group)
+        send = recs[:nb]
+        if send.numel() < nb:  # a smaller buffer than another rank's count: pad (sizes must match)
+            send = torch.cat([send, torch.zeros(nb - send.numel(), dtype=recs.dtype, device=recs.device)])
+        dist.all_gather(gr, send.contiguous(), group=group)
     gc = [m[:-1].astype(np.int32) for m in gm]
     return gc, gr
 

@@ -25,7 +25,7 @@ def _records_for(oracle, casc, frames, params, frame0, rng):
     return a
 
 
-def _worker(rank, world, port, n_frames, out_q):
+def _worker(rank, world, port, n_frames, out_q, tight=False):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -39,7 +39,9 @@ def _worker(rank, world, port, n_frames, out_q):
     start, cnt = shard_range(n_frames, world, rank)
     frames = np.stack([synth.make_frame(320, 240, 500 + start + k) for k in range(cnt)])
     a = _records_for(O, casc, frames, params, start, np.random.default_rng(rank))
-    cap = 1 << 15
+    # tight: each rank's buffer holds exactly its own records, so the rank
+    # with fewer detections sends a buffer shorter than the largest count
+    cap = len(a) if tight else 1 << 15
     buf = np.zeros(cap, RECORD_DTYPE)
     buf[:len(a)] = a
     B = max(shard_range(n_frames, world, r)[1] for r in range(world))
@@ -66,15 +68,15 @@ def test_shard_range_covers_all():
         assert seen == list(range(n))
 
 
-@pytest.mark.parametrize("world", [2])
-def test_gloo_gather_equals_single_process(oracle, world):
+@pytest.mark.parametrize("world,tight", [(2, False), (2, True)])
+def test_gloo_gather_equals_single_process(oracle, world, tight):
     from surfcascade_amd import RECORD_DTYPE, synth
     from surfcascade_amd.dist import merge_records
     n_frames = 5
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + os.getpid() % 1000
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_frames, q)) for r in range(world)]
+    port = 29500 + os.getpid() % 1000 + (7 if tight else 0)
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_frames, q, tight)) for r in range(world)]
     for p in procs:
         p.start()
     got = np.frombuffer(q.get(timeout=120), RECORD_DTYPE)
