@@ -10,5 +10,7 @@ for p in "$SRC"/pmc/*/; do
   n=$(basename "$p"); mkdir -p "$DST/pmc_$n"
   cp "$p/pmc_counter_collection.csv" "$DST/pmc_$n/"
 done
-python3 "$(dirname "$0")/pmc_summary.py" "$SRC/pmc" --json "$(dirname "$0")/pmc_windows.json" > "$DST/pmc_summary.txt"
+# the batch the PMC passes ran (bench.py's default for the config) keys pmc_windows.json
+B=$(python3 -c "import json; print(json.load(open('$SRC/bench_traced.json'))['config']['frames_per_gpu_per_step'])")
+python3 "$(dirname "$0")/pmc_summary.py" "$SRC/pmc" --batch "$B" --json "$(dirname "$0")/pmc_windows.json" > "$DST/pmc_summary.txt"
 sed -i "s|\"source\": \".*\"|\"source\": \"$DST/pmc_*\"|" "$(dirname "$0")/pmc_windows.json"
