@@ -707,7 +707,7 @@ void check_chain(sc_detector *d) {
         unsigned long long pc[16];
         HIPCHK(hipMemcpy(pc, d->d_prof.p, sizeof(pc), hipMemcpyDeviceToHost));
         std::fprintf(stderr, "SC_PROF_CHAIN idle %llu setup %llu eval %llu merge %llu rounds %llu slots %llu "
-                     "deq %llu poll %llu iters %llu lanes %llu thin16 %llu thin32 %llu stages %llu "
+                     "deq %llu poll %llu iters %llu lanes %llu prefilter %llu thin32 %llu stages %llu "
                      "surv %llu need %llu pass %llu\n", pc[0], pc[1], pc[2], pc[3], pc[4], pc[5], pc[6],
                      pc[7], pc[8], pc[9], pc[10], pc[11], pc[12], pc[13], pc[14], pc[15]);
     }

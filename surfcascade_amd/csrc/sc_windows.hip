@@ -203,11 +203,10 @@ struct NoStats {
 };
 struct ItemStats {
     [[maybe_unused]] static constexpr bool on = true;
-    unsigned long long iters = 0, lanes = 0, thin16 = 0, thin32 = 0, stages = 0, surv = 0, need = 0, pass = 0;
+    unsigned long long iters = 0, lanes = 0, pre_cyc = 0, thin32 = 0, stages = 0, surv = 0, need = 0, pass = 0;
     __device__ void iter(int active) {  // one item iteration (a gather round trip)
         iters++;
         lanes += (unsigned)active;
-        thin16 += active <= 16;
         thin32 += active <= 32;
     }
     __device__ void stage(int nsurv) {
@@ -231,6 +230,8 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
     auto slot = [&](unsigned sv) { return (int)(sv >> 16) * stride + (int)(sv & 0xffffu); };
 
     // 1) prefilter; survivors in (row, x) order
+    [[maybe_unused]] unsigned long long t_pre0 = 0;
+    if constexpr (std::remove_reference_t<Stats>::on) t_pre0 = __builtin_amdgcn_s_memtime();
     int nsurv = 0;
     for (int r = 0; r < B.rows(); r++) {
         const int nw = B.width(r), pre_row = B.pre_row_of(r);
@@ -255,6 +256,7 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
         }
     }
     wave_sync();
+    if constexpr (std::remove_reference_t<Stats>::on) stats.pre_cyc += __builtin_amdgcn_s_memtime() - t_pre0;
 
     // 2) cascade, stage by stage over the compacted survivors
     for (int s = 0; s < a.n_stages && nsurv > 0; s++) {
@@ -954,7 +956,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
         atomicAdd(&w.prof[7], c_poll);
         atomicAdd(&w.prof[8], istats.iters);
         atomicAdd(&w.prof[9], istats.lanes);
-        atomicAdd(&w.prof[10], istats.thin16);
+        atomicAdd(&w.prof[10], istats.pre_cyc);
         atomicAdd(&w.prof[11], istats.thin32);
         atomicAdd(&w.prof[12], istats.stages);
         atomicAdd(&w.prof[13], istats.surv);
