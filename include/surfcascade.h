@@ -210,6 +210,8 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
 #define SC_OPT_LDS_WEIGHTS 10 /* -1 auto, 0 weights through the caches, 1 LDS  */
 #define SC_OPT_WGS_PER_CU 11  /* workgroups per CU, 0 = occupancy limit        */
 #define SC_OPT_PROFILE 12     /* chain-kernel phase counters (profiling builds) */
+#define SC_OPT_CHAIN_SEGS 13  /* chain kernel: segments per row (0 auto: 4 for a */
+                              /* one-frame launch, else 8; or 1, 2, 4, 8)      */
 int sc_detector_set_option(sc_detector *d, int option, int64_t value);
 
 /* Enable per-window debug records (grid order) for the next detect calls. */

@@ -125,7 +125,7 @@ struct sc_detector {
     struct Options {
         int full_grid = 0, chunk_min = 0, table_layout = 0, phases = 0, substrips = 0;
         int band_rows = 0, row_order = 2, row_block = 32, chain_chunk = 0;
-        int lds_weights = -1, wgs_per_cu = 0, profile = 0;
+        int lds_weights = -1, wgs_per_cu = 0, profile = 0, chain_segs = 0;
     } opt;
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
@@ -620,7 +620,20 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     ca.st_p = d->d_st_p.p;
     ca.st_s = d->d_st_s.p;
     HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kQueueWords, d->stream));
-    const int seg_max = (g.nx_max + sc::kChainSegs - 1) / sc::kChainSegs;  // chain kernel segments
+    // chain kernel launches: chunks of frames whose tables span < 4 GiB (32-bit
+    // byte offsets); rows cut into 8 segments (one per XCD), or 4 for a
+    // one-frame launch, whose time the segment hand-off chain's fill and
+    // drain dominate (0.73 vs 0.83 ms per 1080p frame; 8 win from 2 frames
+    // on)
+    int chunk = (int)std::max<long long>(1, (1ll << 28) / g.tg.frame4);
+    if (d->opt.chain_chunk > 0) chunk = std::min(chunk, d->opt.chain_chunk);  // SC_OPT_CHAIN_CHUNK
+    auto segs_for = [&](int frames) {  // SC_OPT_CHAIN_SEGS overrides
+        return d->opt.chain_segs ? d->opt.chain_segs : (frames == 1 ? sc::kXcds / 2 : sc::kXcds);
+    };
+    auto seg_max_for = [&](int s) { return (g.nx_max + s - 1) / s; };
+    const int last = n % chunk ? n % chunk : std::min(chunk, n);
+    const int smin = std::min(segs_for(std::min(chunk, n)), segs_for(last));  // widest segment of the call
+    const int seg_max = seg_max_for(smin);
     const bool lazy = d->lazy && sc::chain_lds_bytes(d->K, seg_max, g.n_levels) <= 160 * 1024;
     if (!lazy) {
         timed_begin(d, &e0);
@@ -649,9 +662,6 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     wk.row_max = seg_max;
     if (lazy) {  // the walk drives the cascade: one chain kernel per chunk of frames
         const size_t n_rows = g.rows.size();
-        // table offsets are 32-bit byte offsets from the chunk's first frame
-        int chunk = (int)std::max<long long>(1, (1ll << 28) / g.tg.frame4);
-        if (d->opt.chain_chunk > 0) chunk = std::min(chunk, d->opt.chain_chunk);  // SC_OPT_CHAIN_CHUNK
         d->d_entry.ensure(n_rows * std::min(chunk, n) * sc::kXcds + 1);
         if (d->debug) {  // dumps: unevaluated windows read -2, unvisited 0
             HIPCHK(hipMemsetAsync(d->d_st_p.p, 0xFE, (size_t)g.grid * n, d->stream));
@@ -674,6 +684,9 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             d->err_word = (long long)(n_rows * std::min(chunk, n) * sc::kXcds);
             wc.err = d->d_entry.p + d->err_word;
             wc.frame0 = f0;
+            wc.nseg = segs_for(nc);
+            wc.seg_shift = wc.nseg == 8 ? 0 : wc.nseg == 4 ? 1 : wc.nseg == 2 ? 2 : 3;
+            wc.row_max = seg_max_for(wc.nseg);  // (<= seg_max: the LDS check above)
             if (d->opt.profile) {  // SC_OPT_PROFILE (SC_PROF_CHAIN builds): cumulative phase cycles
                 if (!d->d_prof.p) {
                     d->d_prof.ensure(16);
@@ -1308,6 +1321,11 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
             case SC_OPT_LDS_WEIGHTS: o.lds_weights = range(-1, 1); regeo = false; break;
             case SC_OPT_WGS_PER_CU: o.wgs_per_cu = range(0, 4); regeo = false; break;
             case SC_OPT_PROFILE: o.profile = range(0, 1); regeo = false; break;
+            case SC_OPT_CHAIN_SEGS:
+                o.chain_segs = range(0, sc::kXcds);
+                if (o.chain_segs & (o.chain_segs - 1)) throw Error{SC_ERR_INVALID, "chain_segs: 0, 1, 2, 4 or 8"};
+                regeo = false;
+                break;
             default: throw Error{SC_ERR_INVALID, "unknown option " + std::to_string(option)};
         }
         d->chunk_min = o.chunk_min > 0 ? o.chunk_min : 1 << 30;

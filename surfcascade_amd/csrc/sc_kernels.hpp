@@ -27,13 +27,9 @@ constexpr int kXcds = 8;          // MI355X: 8 XCDs, one L2 each
 constexpr int kQueueStride = 64;  // ints between per-XCD queue words (own 256-B line each)
 constexpr int kMaxSubQ = 8;       // chain kernel: dequeue counters per XCD queue, at most
 constexpr int kQueueWords = kXcds * kMaxSubQ * kQueueStride;  // the queue buffer
-#ifndef SC_NSEG
-#define SC_NSEG 8
-#endif
-// chain kernel: segments per row; XCD x serves segment x / (kXcds / kChainSegs)
-// and, of that segment, the rows of class x % (kXcds / kChainSegs)
-constexpr int kChainSegs = SC_NSEG;
-static_assert(kChainSegs >= 1 && kXcds % kChainSegs == 0, "segments per row divide the XCD count");
+// chain kernel: segments per row, chosen per launch (WalkArgs::nseg, a power
+// of 2 dividing kXcds); XCD x serves segment x / (kXcds / nseg) and, of that
+// segment, the rows of class x % (kXcds / nseg)
 
 struct TableGeom {
     int W, H, step;
@@ -176,6 +172,8 @@ struct WalkArgs {
     int *entry;      // chain kernel: [frame*rows][kXcds] chain entry + 1 per segment (zeroed)
     int *err;        // chain kernel: hand-off timeouts (must stay 0)
     int frame0;      // chain kernel: first frame of this launch (record frame index)
+    int nseg;        // chain kernel: segments per row (8; 4 for one-frame launches)
+    int seg_shift;   // chain kernel: log2(kXcds / nseg)
     unsigned long long *prof;  // chain kernel, SC_PROF_CHAIN builds: phase cycle totals (or null)
 };
 

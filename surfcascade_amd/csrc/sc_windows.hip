@@ -641,7 +641,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
     // a few hundred waves per XCD dequeuing through one atomic word
     // serialise on its line).  A drained sub-queue sends the wave on to the
     // next one, then to the other XCDs' queues.
-    constexpr int kCls = kXcds / kChainSegs;  // row classes per segment
+    const int nsg = w.nseg, sh = w.seg_shift;  // segments per row; XCDs per segment = 1 << sh
     int q = (int)xcc_id(), empty = 0;
     int u = (int)((blockIdx.x / kXcds * kChainWaves + wv) % kSubQ);
     bool drained = false;
@@ -664,10 +664,10 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
         while (!drained) {
             int v = 0;
             if (lane == 0) v = atomicAdd(&a.queues[(q * kSubQ + u) * kQueueStride], 1);
-            v = (__builtin_amdgcn_readfirstlane(v) * kSubQ + u) * kCls + q % kCls;
+            v = ((__builtin_amdgcn_readfirstlane(v) * kSubQ + u) << sh) + (q & ((1 << sh) - 1));
             if (v < n_tasks) {
                 t = v;
-                qq = q / kCls;  // the segment
+                qq = q >> sh;  // the segment
                 rd = w.rows[v % w.n_rows];
                 return true;
             }
@@ -683,8 +683,8 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
     // the chain leaves slot sl's segment at absolute position pos: hand it on
     auto finish = [&](int sl, int pos) {
         if (lane == 0) {
-            if (tq[sl] + 1 < kChainSegs)
-                __hip_atomic_store(&w.entry[(long long)tt[sl] * kChainSegs + tq[sl] + 1], pos + 1,
+            if (tq[sl] + 1 < nsg)
+                __hip_atomic_store(&w.entry[(long long)tt[sl] * nsg + tq[sl] + 1], pos + 1,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (nvis[sl]) atomicAdd(&w.row_visited[tt[sl]], nvis[sl]);
         }
@@ -710,7 +710,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
                 int t, qq;
                 int2 rd;
                 if (dequeue(t, qq, rd)) {
-                    const int nx = Lv[rd.x].nx, nxs = (nx + kChainSegs - 1) / kChainSegs;
+                    const int nx = Lv[rd.x].nx, nxs = (nx + nsg - 1) / nsg;
                     tt[sl] = t;
                     tq[sl] = qq;
                     frame[sl] = t / w.n_rows;
@@ -732,7 +732,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
             for (int sl = 0; sl < kSlots; sl++) {
                 e[sl] = 0;
                 if (st[sl] == 1 && lane == 0)
-                    e[sl] = __hip_atomic_load(&w.entry[(long long)tt[sl] * kChainSegs + tq[sl]], __ATOMIC_RELAXED,
+                    e[sl] = __hip_atomic_load(&w.entry[(long long)tt[sl] * nsg + tq[sl]], __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
             }
 #pragma unroll

@@ -117,6 +117,15 @@ def test_chain_row_orders(sc, oracle, face_cascade, order, block):
                  oracle.Params(n_levels=8), **opts)
 
 
+@pytest.mark.parametrize("segs", ["1", "2", "8"])
+def test_chain_segments_per_row(sc, oracle, face_cascade, segs):
+    """A single frame with other segment counts than its default 4: the
+    evaluated windows, visited set and detections stay the oracle's."""
+    img = _frame(1280, 720, 79)
+    _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=8),
+                 oracle.Params(n_levels=8), chain_segs=int(segs))
+
+
 @pytest.mark.parametrize("lds_weights", [None, "0"])
 def test_pedestrian_64x128(sc, oracle, ped_cascade, lds_weights):
     # lds_weights 0: the cache-read weights variant (models too big for the LDS)
@@ -167,9 +176,14 @@ def test_lazy_grid_wide_rows_and_frame_chunks(sc, oracle, face_cascade):
     assert sum(len(b) for b in batch) > 100
 
 
-def test_batch_equals_single(sc, oracle, face_cascade):
+@pytest.mark.parametrize("segs", [None, "1", "2", "4", "8"])
+def test_batch_equals_single(sc, oracle, face_cascade, segs):
+    """Batches (8 segments per row by default) equal single frames (4 by
+    default) and the oracle; forced segment counts change the schedule only."""
     frames = np.stack([_frame(640, 480, 100 + k) for k in range(4)])
     det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=5))
+    if segs:
+        det.set_option("chain_segs", int(segs))
     batch = det.detect_batch(frames)
     for k in range(4):
         single = det.detect(frames[k])
