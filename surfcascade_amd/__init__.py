@@ -45,7 +45,7 @@ KERNELS = ("rowscan", "colscan", "windows", "walk")
 # layout choices that never change a result bit
 OPTIONS = {"full_grid": 1, "chunk_min": 2, "table_layout": 3, "phases": 4, "substrips": 5,
            "band_rows": 6, "row_order": 7, "row_block": 8, "chain_chunk": 9, "lds_weights": 10,
-           "wgs_per_cu": 11, "profile": 12, "chain_segs": 13}
+           "wgs_per_cu": 11, "profile": 12, "chain_segs": 13, "integral_passes": 14}
 
 # every symbol include/surfcascade.h declares
 EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_model_save",

@@ -125,7 +125,7 @@ struct sc_detector {
     struct Options {
         int full_grid = 0, chunk_min = 0, table_layout = 0, phases = 0, substrips = 0;
         int band_rows = 0, row_order = 2, row_block = 32, chain_chunk = 0;
-        int lds_weights = -1, wgs_per_cu = 0, profile = 0, chain_segs = 0;
+        int lds_weights = -1, wgs_per_cu = 0, profile = 0, chain_segs = 0, integral_passes = 0;
     } opt;
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
@@ -589,7 +589,10 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     timed_end(d, SC_KERNEL_ROWSCAN, e0);
 
     timed_begin(d, &e0);
-    sc::launch_colscan(ra, n, d->stream);
+    // colstrip's 60 waves per frame walk every row: for one or two frames the
+    // row-parallel two-pass form is shorter (SC_OPT_INTEGRAL_PASSES overrides)
+    const bool two_pass = d->opt.integral_passes ? d->opt.integral_passes == 2 : n <= 2;
+    sc::launch_colscan(ra, n, two_pass, d->stream);
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_COLSCAN, e0);
 
@@ -1321,6 +1324,7 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
             case SC_OPT_LDS_WEIGHTS: o.lds_weights = range(-1, 1); regeo = false; break;
             case SC_OPT_WGS_PER_CU: o.wgs_per_cu = range(0, 4); regeo = false; break;
             case SC_OPT_PROFILE: o.profile = range(0, 1); regeo = false; break;
+            case SC_OPT_INTEGRAL_PASSES: o.integral_passes = range(0, 2); regeo = false; break;
             case SC_OPT_CHAIN_SEGS:
                 o.chain_segs = range(0, sc::kXcds);
                 if (o.chain_segs & (o.chain_segs - 1)) throw Error{SC_ERR_INVALID, "chain_segs: 0, 1, 2, 4 or 8"};

@@ -181,15 +181,77 @@ __global__ __launch_bounds__(64) void colstrip_kernel(RowScanArgs a) {
     }
 }
 
+// Small batches (a single frame's colstrip is 60 waves walking 1080 rows:
+// 0.21 ms of latency) split colstrip in two passes over the table:
+//   rowfull : one wave per (frame, row, 64-column strip, half): the same
+//             gradients, in-strip scan and carry as colstrip, writing the
+//             exact row prefix R_y[x+1] (u32 x 4) into the table cell;
+//   colsum  : one wave per (frame, strip, half), lane = column: S += (float)R
+//             down the column in place, loads of the next rows in flight.
+// The f32 operations and their order are colstrip's (S_{y+1} = S_y + R_y);
+// the table is written twice and read once, so large batches keep colstrip.
+__global__ __launch_bounds__(64) void rowfull_kernel(RowScanArgs a) {
+    const int s = blockIdx.x >> 1, h = blockIdx.x & 1, y = blockIdx.y, frame = blockIdx.z, lane = threadIdx.x;
+    const TableGeom g = a.g;
+    const int W = g.W, H = g.H, ns = (W + kStrip - 1) / kStrip;
+    const int x = s * 2 * kStrip + lane;
+    const bool live = x < W;
+    const uint8_t *img = a.frames + (long long)frame * a.frame_bytes;
+    const Px4 px = load_px(img, a.stride, W, H, y, live ? x : W - 1, h);
+    uint2 p = live ? grad_packed(px) : make_uint2(0u, 0u);
+    p.x = wave_scan(p.x);
+    p.y = wave_scan(p.y);
+    const uint4 c = reinterpret_cast<const uint4 *>(a.carry)[(((long long)frame * H + y) * ns + 2 * s) * 2 + h];
+    const uint4 R = make_uint4(c.x + (p.x & 0xffffu), c.y + (p.x >> 16), c.z + (p.y & 0xffffu), c.w + (p.y >> 16));
+    if (live)
+        reinterpret_cast<uint4 *>(a.table)[(long long)frame * g.frame4 + (long long)(y + 1) * g.rowp + g.at(x + 1, h)] = R;
+}
+
+constexpr int kSumAhead = 16;  // colsum: rows of loads in flight
+__global__ __launch_bounds__(64) void colsum_kernel(RowScanArgs a) {
+    const int s = blockIdx.x >> 1, h = blockIdx.x & 1, frame = blockIdx.y, lane = threadIdx.x;
+    const TableGeom g = a.g;
+    const int W = g.W, H = g.H;
+    const int x = s * 2 * kStrip + lane;
+    if (x >= W) return;  // (no cross-lane work in this pass)
+    float4 *cellp = a.table + (long long)frame * g.frame4 + g.at(x + 1, h) + g.rowp;  // table row 1
+    const uint4 *rp = reinterpret_cast<const uint4 *>(cellp);
+    float S0 = 0.0f, S1 = 0.0f, S2 = 0.0f, S3 = 0.0f;
+    uint4 ra[kSumAhead];
+#pragma unroll
+    for (int k = 0; k < kSumAhead; k++) ra[k] = rp[(long long)min(k, H - 1) * g.rowp];
+    for (int y0 = 0; y0 < H; y0 += kSumAhead) {
+        uint4 rb[kSumAhead];
+#pragma unroll
+        for (int k = 0; k < kSumAhead; k++) rb[k] = rp[(long long)min(y0 + kSumAhead + k, H - 1) * g.rowp];
+#pragma unroll
+        for (int k = 0; k < kSumAhead; k++) {
+            const int y = y0 + k;
+            S0 = S0 + (float)ra[k].x;  // the f32 column step, colstrip's order
+            S1 = S1 + (float)ra[k].y;
+            S2 = S2 + (float)ra[k].z;
+            S3 = S3 + (float)ra[k].w;
+            if (y < H) cellp[(long long)y * g.rowp] = make_float4(S0, S1, S2, S3);
+        }
+#pragma unroll
+        for (int k = 0; k < kSumAhead; k++) ra[k] = rb[k];
+    }
+}
+
 }  // namespace
 
 void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
     hipLaunchKernelGGL(rowcarry_kernel, dim3(a.g.H, n_frames), dim3(64), 0, s, a);
 }
 
-void launch_colscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
+void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s) {
     const int ns64 = (a.g.W + 2 * kStrip - 1) / (2 * kStrip);
-    hipLaunchKernelGGL(colstrip_kernel, dim3(ns64 * 2, n_frames), dim3(64), 0, s, a);
+    if (two_pass) {
+        hipLaunchKernelGGL(rowfull_kernel, dim3(ns64 * 2, a.g.H, n_frames), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(colsum_kernel, dim3(ns64 * 2, n_frames), dim3(64), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(colstrip_kernel, dim3(ns64 * 2, n_frames), dim3(64), 0, s, a);
+    }
 }
 
 }  // namespace sc

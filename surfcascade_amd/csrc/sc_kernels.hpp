@@ -220,7 +220,8 @@ void launch_features(const FeatureArgs &a, hipStream_t s);
 
 // integral pass 1 (rowcarry) and pass 2 (colstrip), sc_integral.hip
 void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s);
-void launch_colscan(const RowScanArgs &a, int n_frames, hipStream_t s);
+// two_pass: rowfull + colsum (small batches), else colstrip
+void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s);
 // Per-detector launch configuration: the device's CU count (queried once
 // per detector, no process-wide cache) and the SC_OPT_* launch options.
 struct LaunchCfg {

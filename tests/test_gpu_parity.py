@@ -29,12 +29,15 @@ def _det_set(arr):
                    int(r["stage"]), float(r["score"])) for r in arr)
 
 
+@pytest.mark.parametrize("passes", ["1", "2"])
 @pytest.mark.parametrize("layout", ["0", "1"])
 @pytest.mark.parametrize("W,H,seed", [(640, 480, 1), (1920, 1080, 1000), (257, 131, 7), (2, 2, 3),
                                       (3000, 67, 5)])
-def test_integral_bit_exact(sc, oracle, W, H, seed, layout):
+def test_integral_bit_exact(sc, oracle, W, H, seed, layout, passes):
+    """Both integral forms (colstrip; rowfull + colsum, the small-batch default)."""
     img = _frame(W, H, seed)
     det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1)).set_option("table_layout", int(layout))
+    det.set_option("integral_passes", int(passes))
     det.detect(img)  # frames smaller than the window: no rows, integral still built
     T = det.dump_integral(W, H)
     ref = oracle.integral(img)
