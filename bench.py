@@ -36,7 +36,8 @@ MODELS = os.path.join(ROOT, "surfcascade_amd", "models")
 # (256 frames / 8 GPUs = 32), so `--gpus 8` runs exactly C3; the chain
 # kernel's per-launch fill and drain cost 4.5 % more per frame at 16
 # (the single-frame time is reported beside).  C4 runs
-# 8 4K frames per step for the same reason (6.49 vs 6.18 G windows/s at 4).
+# 8 4K frames per step for the same reason (6.49 vs 6.18 G windows/s at 4),
+# C5 32 like C2 (3.81 vs 3.58 at 16).
 CONFIGS = {
     "C2": dict(width=1920, height=1080, levels=24, batch=32, model="face40_synth.cfg",
                pedestrian=False,
@@ -48,7 +49,7 @@ CONFIGS = {
                metric="detection windows/sec on 4K 32-scale pyramid",
                desc="C4: %dx%d frames, %d-level window pyramid (l=70..%d), 40x40 face cascade "
                     "10 stages / 190 weak LR"),
-    "C5": dict(width=1920, height=1080, levels=23, batch=16, model="ped64x128_synth.cfg",
+    "C5": dict(width=1920, height=1080, levels=23, batch=32, model="ped64x128_synth.cfg",
                pedestrian=True,
                metric="detection windows/sec, 64x128 pedestrian cascade on 1080p 23-scale pyramid",
                desc="C5: %dx%d frames, %d-level window pyramid (l=64..%d, h=2l), 64x128 pedestrian "
