@@ -120,6 +120,19 @@ def test_chain_row_orders(sc, oracle, face_cascade, order, block):
                  oracle.Params(n_levels=8), **opts)
 
 
+@pytest.mark.parametrize("n", [2, 3])
+def test_integral_batch_frames(sc, oracle, n):
+    """Every frame of a batch: 2 frames take the two-pass integral (rowfull +
+    colsum), 3 take colstrip; odd sizes, so strips and rows end ragged."""
+    frames = np.stack([_frame(577, 301, 900 + k) for k in range(n)])
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=2))
+    det.set_debug(True)
+    det.detect_batch(frames)
+    for k in range(n):
+        T = det.dump_integral(577, 301, frame=k)
+        assert T.view(np.uint32).tobytes() == oracle.integral(frames[k]).view(np.uint32).tobytes()
+
+
 @pytest.mark.parametrize("segs", ["1", "2", "8"])
 def test_chain_segments_per_row(sc, oracle, face_cascade, segs):
     """A single frame with other segment counts than its default 4: the
