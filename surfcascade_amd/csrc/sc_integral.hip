@@ -128,10 +128,37 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
     return v;
 }
 
+#ifndef SC_COL_XCD
+#define SC_COL_XCD 1
+#endif
+// Which (frame, half, strip) a column-walk workgroup takes.  The hardware
+// deals workgroup b (linear id) to XCD b % kXcds; with SC_COL_XCD each XCD
+// gets a contiguous run of (frame, half, strip) ids instead, strip fastest,
+// so the 128-B lines two neighbouring strips share at a phase-plane run's
+// ends are written through one L2 (adjacent ids on two XCDs leave two
+// partial dirty copies of each such line).
+struct ColBlock {
+    int s, h, frame;
+};
+__device__ __forceinline__ ColBlock col_block() {
+    const int ns64 = gridDim.x >> 1;
+#if SC_COL_XCD
+    const int nb = gridDim.x * gridDim.y, b = blockIdx.x + blockIdx.y * gridDim.x;
+    const int x = b % kXcds, q = nb / kXcds, r = nb % kXcds;
+    const int lb = x * q + min(x, r) + b / kXcds;  // a bijection onto [0, nb)
+    const int f = lb / gridDim.x, rem = lb - f * gridDim.x;
+    return ColBlock{rem % ns64, rem / ns64, f};
+#else
+    (void)ns64;
+    return ColBlock{(int)blockIdx.x >> 1, (int)blockIdx.x & 1, (int)blockIdx.y};
+#endif
+}
+
 // One wave per (frame, 64-column strip, channel half): lane = column, so a
 // row's stores are long runs within each phase plane of the half.
 __global__ __launch_bounds__(64) void colstrip_kernel(RowScanArgs a) {
-    const int s = blockIdx.x >> 1, h = blockIdx.x & 1, frame = blockIdx.y, lane = threadIdx.x;
+    const ColBlock cb_ = col_block();
+    const int s = cb_.s, h = cb_.h, frame = cb_.frame, lane = threadIdx.x;
     const TableGeom g = a.g;
     const int W = g.W, H = g.H, ns = (W + kStrip - 1) / kStrip;  // carries per 32-px strip
     const int x = s * 2 * kStrip + lane;
@@ -209,7 +236,8 @@ __global__ __launch_bounds__(64) void rowfull_kernel(RowScanArgs a) {
 
 constexpr int kSumAhead = 16;  // colsum: rows of loads in flight
 __global__ __launch_bounds__(64) void colsum_kernel(RowScanArgs a) {
-    const int s = blockIdx.x >> 1, h = blockIdx.x & 1, frame = blockIdx.y, lane = threadIdx.x;
+    const ColBlock cb_ = col_block();
+    const int s = cb_.s, h = cb_.h, frame = cb_.frame, lane = threadIdx.x;
     const TableGeom g = a.g;
     const int W = g.W, H = g.H;
     const int x = s * 2 * kStrip + lane;
