@@ -229,8 +229,11 @@ void build_geometry(sc_detector *d, int W, int H) {
     ng.W = W;
     ng.H = H;
     ng.step = ref_step(p);
-    ng.n_levels = ref_levels(W, H, p);
-    if (ng.n_levels < 0 || ng.n_levels > 256) throw Error{SC_ERR_INVALID, "bad level count"};
+    // a frame smaller than the base window gives a negative count from the
+    // formula: the reference's inclusive level loop (ObjDetector.cpp:178)
+    // then runs no level, and so does the scan here
+    ng.n_levels = std::max(0, ref_levels(W, H, p));
+    if (ng.n_levels > 256) throw Error{SC_ERR_INVALID, "bad level count"};
     {   // phase-split table geometry (sc_kernels.hpp)
         sc::TableGeom &t = ng.tg;
         t.W = W;

@@ -147,3 +147,17 @@ def test_mine_batch_device_first_round(sc, oracle):
     assert list(counts) == rc and sum(rc) > cap
     f = feats.view(cap, m.n_patches, 32)[:len(wins)].cpu().numpy()
     _check((wins, f, sum(rc)), (rw, rf, sum(rc)))
+
+
+@pytest.mark.parametrize("W,H", [(30, 60), (60, 39), (40, 40), (44, 300)])
+def test_first_round_small_images(sc, oracle, W, H):
+    """Negative images at and below the 40-px template: the scale count
+    (int)min(log(W/40f)/log 1.1, log(H/40f)/log 1.1) is negative below 40 px
+    and the reference's inclusive scale loop (DenseSURFFeatureExtractor.cpp:
+    142-145) runs no scale; at 40 px exactly one window."""
+    img = _frame(W, H, 31 + W + H)
+    m = sc.Miner(None)
+    got = m.mine(img, 64)
+    ref = oracle.mine(oracle.integral(img), oracle.empty_cascade(), 64)
+    _check(got, ref)
+    assert (got[2] == 0) == (min(W, H) < 40)

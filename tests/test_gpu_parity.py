@@ -337,3 +337,27 @@ def test_jpeg_to_detections(sc, oracle, face_cascade):
     det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=4))
     ref, _ = oracle.detect(oracle.integral(img), face_cascade, oracle.Params(n_levels=4))
     assert _det_set(det.detect(img)) == _det_set(ref)
+
+
+@pytest.mark.parametrize("W,H", [(60, 50), (70, 70), (71, 400), (400, 71), (76, 90), (69, 1000)])
+def test_small_frames_default_levels(sc, oracle, face_cascade, W, H):
+    """Frames at and below the base window (ObjDetector.cpp:174-186: the level
+    count (int)min(log(W/70)/log 1.1, log(H/70)/log 1.1) + 1 is 0 below 70 px,
+    one row / one column of windows at exactly 70): detections, scores and
+    visited counts equal the oracle's, with a permissive cascade so windows
+    that exist reach the last stage."""
+    from surfcascade_amd import synth
+    c = face_cascade
+    theta = np.full(c.n_stages, 0.3, np.float32)
+    text = synth.write_cfg(synth.cascade_tree(c.n_weak, theta, c.patch_index, c.w, c.bias))
+    casc_or = oracle.cascade_from_cfg(text)
+    img = _frame(W, H, 4242 + W + H)
+    ref, nvis = oracle.detect(oracle.integral(img), casc_or, oracle.Params())
+    det = sc.Detector(sc.Model.parse(text), sc.ScanParams())
+    got = det.detect(img)
+    assert _det_set(got) == _det_set(ref)
+    assert det.info("visited") == nvis
+    if min(W, H) < 70:
+        assert nvis == 0 and len(ref) == 0
+    else:
+        assert nvis > 0 and len(ref) > 0
