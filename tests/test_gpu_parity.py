@@ -361,3 +361,16 @@ def test_small_frames_default_levels(sc, oracle, face_cascade, W, H):
         assert nvis == 0 and len(ref) == 0
     else:
         assert nvis > 0 and len(ref) > 0
+
+
+@pytest.mark.parametrize("base,step,pk,ss,full", [(48, 0, 4.0, 0.6, None), (100, 7, 8.0, 0.4, None),
+                                                  (40, 1, 6.0, 0.5, None), (48, 0, 4.0, 0.6, "1")])
+def test_grid_parity_scan_parameters(sc, oracle, face_cascade, base, step, pk, ss, full):
+    """sc_scan_params beyond the reference's constants (ObjDetector.cpp:104,
+    139, 188, 214): window base, row/column step (0 = base/20), prefilter
+    factor and the adaptive-stride score threshold, on both window kernels."""
+    img = _frame(480, 360, 90 + base + step)
+    _grid_parity(sc, oracle, face_cascade, FACE_CFG, img,
+                 sc.ScanParams(base_len=base, step=step, prefilter_k=pk, stride_score=ss, n_levels=6),
+                 oracle.Params(base_len=base, step=step, prefilter_k=pk, stride_score=ss, n_levels=6),
+                 full_grid=int(full or 0))
