@@ -44,8 +44,8 @@ def test_integral_bit_exact(sc, oracle, W, H, seed, layout, passes):
     assert T.view(np.uint32).tobytes() == ref.view(np.uint32).tobytes()
 
 
-def _grid_parity(sc, oracle, cascade, cfg, img, params_sc, params_or, **opts):
-    det = sc.Detector(cfg, params_sc).set_options(**opts)
+def _grid_parity(sc, oracle, cascade, cfg, img, params_sc, params_or, model_text=None, **opts):
+    det = sc.Detector(sc.Model.parse(model_text) if model_text else cfg, params_sc).set_options(**opts)
     det.set_debug(True)
     wins = det.detect(img)
     p, s, v = det.dump_grid()
@@ -374,3 +374,22 @@ def test_grid_parity_scan_parameters(sc, oracle, face_cascade, base, step, pk, s
                  sc.ScanParams(base_len=base, step=step, prefilter_k=pk, stride_score=ss, n_levels=6),
                  oracle.Params(base_len=base, step=step, prefilter_k=pk, stride_score=ss, n_levels=6),
                  full_grid=int(full or 0))
+
+
+@pytest.mark.parametrize("full", [None, "1"])
+def test_grid_parity_large_stages(sc, oracle, face_cascade, full):
+    """A cascade whose stages outgrow the per-wave item buffer (700 weak
+    classifiers: the one-lane-per-window stage path) and whose weights do not
+    fit the LDS (2 200 weak: weights read through the caches)."""
+    from surfcascade_amd import synth
+    c = face_cascade
+    n_weak = [700, 1500]
+    idx = np.arange(sum(n_weak)) % len(c.patch_index)
+    text = synth.write_cfg(synth.cascade_tree(n_weak, np.array([0.5, 0.5], np.float32),
+                                              c.patch_index[idx], c.w[idx], c.bias[idx]))
+    casc = oracle.cascade_from_cfg(text)
+    img = _frame(320, 240, 3)
+    det_params = sc.ScanParams(n_levels=2)
+    _, p = _grid_parity(sc, oracle, casc, None, img, det_params, oracle.Params(n_levels=2),
+                        model_text=text, full_grid=int(full or 0))
+    assert (p == 0).any() and (p == 2).any()  # stage 0 rejects some windows, some pass both
