@@ -393,3 +393,37 @@ def test_grid_parity_large_stages(sc, oracle, face_cascade, full):
     _, p = _grid_parity(sc, oracle, casc, None, img, det_params, oracle.Params(n_levels=2),
                         model_text=text, full_grid=int(full or 0))
     assert (p == 0).any() and (p == 2).any()  # stage 0 rejects some windows, some pass both
+
+
+@pytest.mark.parametrize("kind", ["checker", "noise", "zeros", "white", "stripes"])
+@pytest.mark.parametrize("passes", ["1", "2"])
+def test_integral_extreme_content(sc, oracle, kind, passes):
+    """Content at the ends of the value range (T2bFilter + integral_,
+    DenseSURFFeatureExtractor.cpp:73-76, 199-349): a one-pixel 0/255
+    checkerboard gives the largest gradients everywhere (in-strip sums at
+    64 x 255, table values near 5e8, far past 2^24), noise, flat frames and
+    vertical stripes (every column's dx saturated, dy zero)."""
+    W, H = 1920, 1080
+    yy, xx = np.mgrid[0:H, 0:W]
+    img = {"checker": ((xx + yy) & 1) * 255,
+           "noise": np.random.default_rng(7).integers(0, 256, (H, W)),
+           "zeros": np.zeros((H, W)),
+           "white": np.full((H, W), 255),
+           "stripes": (xx & 1) * 255}[kind].astype(np.uint8)
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1)).set_option("integral_passes", int(passes))
+    det.detect(img)
+    T = det.dump_integral(W, H)
+    ref = oracle.integral(img)
+    assert T.view(np.uint32).tobytes() == ref.view(np.uint32).tobytes()
+
+
+@pytest.mark.parametrize("kind", ["checker", "noise"])
+def test_grid_parity_extreme_content(sc, oracle, face_cascade, kind):
+    """Per-window bits, visited set and detections on frames where every
+    window passes the prefilter (noise) or every gradient saturates (checker)."""
+    W, H = 640, 480
+    yy, xx = np.mgrid[0:H, 0:W]
+    img = (((xx + yy) & 1) * 255 if kind == "checker"
+           else np.random.default_rng(11).integers(0, 256, (H, W))).astype(np.uint8)
+    _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=5),
+                 oracle.Params(n_levels=5))
