@@ -96,7 +96,10 @@ int sc_detector_create_from_model(const sc_model *m, const sc_scan_params *p,
 void sc_detector_destroy(sc_detector *d);
 
 /* One host frame -> raw windows (sorted).  *n_out = total count even when it
- * exceeds capacity (then SC_ERR_CAPACITY and the first `capacity` stored). */
+ * exceeds capacity (then SC_ERR_CAPACITY and the first `capacity` stored).
+ * Frames are 2x2 .. 32767x32767; one smaller than the base window scans no
+ * level and returns no window (the reference's level loop runs zero times,
+ * ObjDetector.cpp:174-178). */
 int sc_detect(sc_detector *d, const uint8_t *gray, int w, int h,
               int stride_bytes, sc_window *out, int capacity, int *n_out);
 /* n host frames of one size.  out holds all frames' windows back to back;
