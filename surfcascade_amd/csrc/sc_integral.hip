@@ -266,6 +266,45 @@ __global__ __launch_bounds__(64) void colsum_kernel(RowScanArgs a) {
     }
 }
 
+#ifndef SC_COLSUM4
+#define SC_COLSUM4 1
+#endif
+// colsum with one lane per (column, channel): 4 waves per (strip, half), each
+// 16 columns x 4 channels, one dword per row and lane, so a lane keeps 4x
+// the rows of loads in flight in the same registers (the walk is bound by
+// the load latency: 120 walks for a 1080p frame, one per SIMD at most).
+constexpr int kSumAhead4 = 48;
+__global__ __launch_bounds__(64) void colsum4_kernel(RowScanArgs a) {
+    const int nb = gridDim.x * gridDim.y, b = blockIdx.x + blockIdx.y * gridDim.x;
+    const int xq = b % kXcds, q = nb / kXcds, r = nb % kXcds;
+    const int lb = xq * q + min(xq, r) + b / kXcds;  // XCD-aware: neighbours through one L2
+    const int frame = lb / gridDim.x, rem = lb - frame * gridDim.x;
+    const int s = rem >> 3, h = (rem >> 2) & 1, sub = rem & 3, lane = threadIdx.x;
+    const TableGeom g = a.g;
+    const int W = g.W, H = g.H;
+    const int x = s * 2 * kStrip + sub * 16 + (lane >> 2), ch = lane & 3;
+    if (x >= W) return;  // (no cross-lane work in this pass)
+    float *cellp = reinterpret_cast<float *>(a.table + (long long)frame * g.frame4 + g.at(x + 1, h) + g.rowp) + ch;
+    const uint32_t *rp = reinterpret_cast<const uint32_t *>(cellp);
+    const long long rs = (long long)g.rowp * 4;  // floats per table row
+    float S = 0.0f;
+    uint32_t ra[kSumAhead4];
+#pragma unroll
+    for (int k = 0; k < kSumAhead4; k++) ra[k] = rp[min(k, H - 1) * rs];
+    for (int y0 = 0; y0 < H; y0 += kSumAhead4) {
+        uint32_t rb[kSumAhead4];
+#pragma unroll
+        for (int k = 0; k < kSumAhead4; k++) rb[k] = rp[min(y0 + kSumAhead4 + k, H - 1) * rs];
+#pragma unroll
+        for (int k = 0; k < kSumAhead4; k++) {
+            S = S + (float)ra[k];  // the f32 column step, colstrip's order
+            if (y0 + k < H) cellp[(y0 + k) * rs] = S;
+        }
+#pragma unroll
+        for (int k = 0; k < kSumAhead4; k++) ra[k] = rb[k];
+    }
+}
+
 }  // namespace
 
 void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
@@ -276,7 +315,10 @@ void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream
     const int ns64 = (a.g.W + 2 * kStrip - 1) / (2 * kStrip);
     if (two_pass) {
         hipLaunchKernelGGL(rowfull_kernel, dim3(ns64 * 2, a.g.H, n_frames), dim3(64), 0, s, a);
-        hipLaunchKernelGGL(colsum_kernel, dim3(ns64 * 2, n_frames), dim3(64), 0, s, a);
+        if (SC_COLSUM4)
+            hipLaunchKernelGGL(colsum4_kernel, dim3(ns64 * 8, n_frames), dim3(64), 0, s, a);
+        else
+            hipLaunchKernelGGL(colsum_kernel, dim3(ns64 * 2, n_frames), dim3(64), 0, s, a);
     } else {
         hipLaunchKernelGGL(colstrip_kernel, dim3(ns64 * 2, n_frames), dim3(64), 0, s, a);
     }
