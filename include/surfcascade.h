@@ -215,7 +215,7 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
 #define SC_OPT_PROFILE 12     /* chain-kernel phase counters (profiling builds) */
 #define SC_OPT_CHAIN_SEGS 13  /* chain kernel: segments per row (0 auto: 4 for a */
                               /* one-frame launch, else 8; or 1, 2, 4, 8)      */
-#define SC_OPT_INTEGRAL_PASSES 14 /* integral: 0 auto (two passes up to 2     */
+#define SC_OPT_INTEGRAL_PASSES 14 /* integral: 0 auto (two passes up to 3     */
                               /* frames), 1 colstrip, 2 rowfull + colsum       */
 int sc_detector_set_option(sc_detector *d, int option, int64_t value);
 

@@ -120,10 +120,11 @@ def test_chain_row_orders(sc, oracle, face_cascade, order, block):
                  oracle.Params(n_levels=8), **opts)
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 4])
 def test_integral_batch_frames(sc, oracle, n):
-    """Every frame of a batch: 2 frames take the two-pass integral (rowfull +
-    colsum), 3 take colstrip; odd sizes, so strips and rows end ragged."""
+    """Every frame of a batch: 2 and 3 frames take the two-pass integral
+    (rowfull + colsum), 4 take colstrip; odd sizes, so strips and rows end
+    ragged."""
     frames = np.stack([_frame(577, 301, 900 + k) for k in range(n)])
     det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=2))
     det.set_debug(True)
