@@ -592,7 +592,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     timed_end(d, SC_KERNEL_ROWSCAN, e0);
 
     timed_begin(d, &e0);
-    // colstrip's 60 waves per frame walk every row: for one or two frames the
+    // colstrip's 60 waves per frame walk every row: for up to three frames the
     // row-parallel two-pass form is shorter (SC_OPT_INTEGRAL_PASSES overrides)
     const bool two_pass = d->opt.integral_passes ? d->opt.integral_passes == 2 : n <= 3;
     sc::launch_colscan(ra, n, two_pass, d->stream);
