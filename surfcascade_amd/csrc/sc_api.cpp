@@ -582,9 +582,41 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     build_geometry(d, W, H);
     ensure_buffers(d, n);
     const Geometry &g = d->geo;
-    HIPCHK(hipMemsetAsync(d_counts, 0, sizeof(int) * (n + 1), d->stream));
+    // chain kernel launches: chunks of frames whose tables span < 4 GiB (32-bit
+    // byte offsets); rows cut into 8 segments (one per XCD), or 4 for a
+    // one-frame launch, whose time the segment hand-off chain's fill and
+    // drain dominate (0.73 vs 0.83 ms per 1080p frame; 8 win from 2 frames
+    // on, DESIGN.md section 5)
+    int chunk = (int)std::max<long long>(1, (1ll << 28) / g.tg.frame4);
+    if (d->opt.chain_chunk > 0) chunk = std::min(chunk, d->opt.chain_chunk);  // SC_OPT_CHAIN_CHUNK
+    auto segs_for = [&](int frames) {  // SC_OPT_CHAIN_SEGS overrides
+        return d->opt.chain_segs ? d->opt.chain_segs : (frames == 1 ? sc::kXcds / 2 : sc::kXcds);
+    };
+    auto seg_max_for = [&](int s) { return (g.nx_max + s - 1) / s; };
+    const int last = n % chunk ? n % chunk : std::min(chunk, n);
+    const int smin = std::min(segs_for(std::min(chunk, n)), segs_for(last));  // widest segment of the call
+    const int seg_max = seg_max_for(smin);
+    const bool lazy = d->lazy && sc::chain_lds_bytes(d->K, seg_max, g.n_levels) <= 160 * 1024;
+    const size_t n_rows = g.rows.size();
+    const bool chain = n_rows > 0 && lazy && !d->miner;
+    if (chain) d->d_entry.ensure(n_rows * std::min(chunk, n) * sc::kXcds + 1);
 
-    sc::RowScanArgs ra{d_frames, (long long)H * stride, stride, d->d_table.p, g.tg, d->d_carry.p};
+    sc::RowScanArgs ra{d_frames, (long long)H * stride, stride, d->d_table.p, g.tg, d->d_carry.p, {}, {}};
+    // zeroed by rowcarry (stream order: before every kernel that uses them):
+    // the output counters, the task queues, the visited counts and the first
+    // chunk's hand-off words
+    ra.zero[0] = d_counts;
+    ra.zero_n[0] = n + 1;
+    if (n_rows > 0) {
+        ra.zero[1] = d->d_queues.p;
+        ra.zero_n[1] = sc::kQueueWords;
+    }
+    if (chain) {
+        ra.zero[2] = reinterpret_cast<int *>(d->d_visited.p);
+        ra.zero_n[2] = (long long)n_rows * n;
+        ra.zero[3] = d->d_entry.p;
+        ra.zero_n[3] = (long long)n_rows * std::min(chunk, n) * sc::kXcds + 1;
+    }
     hipEvent_t e0 = nullptr;
     timed_begin(d, &e0);
     sc::launch_rowscan(ra, n, d->stream);
@@ -625,22 +657,6 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     ca.queues = d->d_queues.p;
     ca.st_p = d->d_st_p.p;
     ca.st_s = d->d_st_s.p;
-    HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kQueueWords, d->stream));
-    // chain kernel launches: chunks of frames whose tables span < 4 GiB (32-bit
-    // byte offsets); rows cut into 8 segments (one per XCD), or 4 for a
-    // one-frame launch, whose time the segment hand-off chain's fill and
-    // drain dominate (0.73 vs 0.83 ms per 1080p frame; 8 win from 2 frames
-    // on, DESIGN.md section 5)
-    int chunk = (int)std::max<long long>(1, (1ll << 28) / g.tg.frame4);
-    if (d->opt.chain_chunk > 0) chunk = std::min(chunk, d->opt.chain_chunk);  // SC_OPT_CHAIN_CHUNK
-    auto segs_for = [&](int frames) {  // SC_OPT_CHAIN_SEGS overrides
-        return d->opt.chain_segs ? d->opt.chain_segs : (frames == 1 ? sc::kXcds / 2 : sc::kXcds);
-    };
-    auto seg_max_for = [&](int s) { return (g.nx_max + s - 1) / s; };
-    const int last = n % chunk ? n % chunk : std::min(chunk, n);
-    const int smin = std::min(segs_for(std::min(chunk, n)), segs_for(last));  // widest segment of the call
-    const int seg_max = seg_max_for(smin);
-    const bool lazy = d->lazy && sc::chain_lds_bytes(d->K, seg_max, g.n_levels) <= 160 * 1024;
     if (!lazy) {
         timed_begin(d, &e0);
         sc::launch_cascade(ca, launch_cfg(d), d->stream);
@@ -667,14 +683,11 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     wk.dbg_v = d->debug ? d->d_dbg_v.p : nullptr;
     wk.row_max = seg_max;
     if (lazy) {  // the walk drives the cascade: one chain kernel per chunk of frames
-        const size_t n_rows = g.rows.size();
-        d->d_entry.ensure(n_rows * std::min(chunk, n) * sc::kXcds + 1);
         if (d->debug) {  // dumps: unevaluated windows read -2, unvisited 0
             HIPCHK(hipMemsetAsync(d->d_st_p.p, 0xFE, (size_t)g.grid * n, d->stream));
             HIPCHK(hipMemsetAsync(d->d_st_s.p, 0, sizeof(float) * (size_t)g.grid * n, d->stream));
             HIPCHK(hipMemsetAsync(d->d_dbg_v.p, 0, (size_t)g.grid * n, d->stream));
         }
-        HIPCHK(hipMemsetAsync(d->d_visited.p, 0, sizeof(unsigned) * n_rows * n, d->stream));
         timed_begin(d, &e0);
         for (int f0 = 0; f0 < n; f0 += chunk) {
             const int nc = std::min(chunk, n - f0);
@@ -700,10 +713,10 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
                 }
                 wc.prof = d->d_prof.p;
             }
-            HIPCHK(hipMemsetAsync(d->d_entry.p, 0, sizeof(int) * (n_rows * nc * sc::kXcds + 1) , d->stream));
-            if (f0 > 0)
-                HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kQueueWords,
-                                      d->stream));
+            if (f0 > 0) {  // (the first chunk's were cleared by rowcarry)
+                HIPCHK(hipMemsetAsync(d->d_entry.p, 0, sizeof(int) * (n_rows * nc * sc::kXcds + 1), d->stream));
+                HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kQueueWords, d->stream));
+            }
             sc::launch_chain(cc, wc, launch_cfg(d), d->stream);
             HIPCHK(hipGetLastError());
         }

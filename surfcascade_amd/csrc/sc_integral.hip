@@ -84,6 +84,13 @@ __global__ __launch_bounds__(64) void rowcarry_kernel(RowScanArgs a) {
     const int h = lane >> 5, c = lane & 31;
     const TableGeom g = a.g;
     const int W = g.W, H = g.H, ns = (W + kStrip - 1) / kStrip;
+    {   // the step's zeroed int arrays, grid-strided over the workgroups
+        const long long nt = (long long)gridDim.x * gridDim.y * 64;
+        const long long i0 = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            for (long long i = i0; i < a.zero_n[k]; i += nt) a.zero[k][i] = 0;
+    }
     const uint8_t *img = a.frames + (long long)frame * a.frame_bytes;
     float4 *tab = a.table + (long long)frame * g.frame4;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);

@@ -108,6 +108,11 @@ struct RowScanArgs {
     float4 *table;
     TableGeom g;
     uint32_t *carry;        // [frame][H][ceil(W/kStrip)][8] exclusive strip prefixes
+    // int arrays the step needs zeroed (counters, queues, hand-off words):
+    // rowcarry's workgroups clear them on the way instead of one fill
+    // dispatch each
+    int *zero[4];
+    long long zero_n[4];
 };
 
 // Cascade kernel: persistent workgroups of 4 independent waves; a task is
