@@ -10,6 +10,14 @@ records (RCCL all_gather when N > 1).  value = stride-3 grid windows of all
 frames of all ranks / max-over-ranks wall time.  Prints one JSON line (rank 0).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2|C4|C5] [--batch B]
+
+--gpus N > 1 without a torch.distributed environment (WORLD_SIZE unset)
+starts the N ranks itself -- `python -m torch.distributed.run --nproc-per-node
+N --master-addr 127.0.0.1 bench.py ...` as a child process, before anything
+touches a GPU -- and exits with its status; a rank that finds WORLD_SIZE !=
+--gpus, or fewer visible GPUs than ranks, exits non-zero instead of measuring
+fewer GPUs.  (--stub: a CPU stand-in for the detector, gloo backend -- the
+CPU test of this launcher, tests/test_bench_launch.py; never a measurement.)
 """
 from __future__ import annotations
 
@@ -81,6 +89,8 @@ def parse():
                     help="steps of the batch-1 (single-frame) latency leg (0: skip)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="sc_detector_set_option (tuning / A-B runs; never changes results)")
+    ap.add_argument("--stub", action="store_true",
+                    help="test only: CPU stand-in detector + gloo (launcher test, not a measurement)")
     a = ap.parse_args()
     c = CONFIGS[a.config]
     if a.batch is None and a.shard == "grid":
@@ -165,24 +175,125 @@ def cpu_baseline(frames, model_path, levels, seconds, pedestrian=False):
             "cgroup_cpu_quota": quota, "cpu_model": cpu_model()}
 
 
+def launch_ranks(args):
+    """--gpus N > 1 outside torch.distributed: run N ranks of this script under
+    torch.distributed.run (one process per GPU, rendezvous on 127.0.0.1) as a
+    child process -- nothing here has touched a GPU -- and return its exit
+    status (non-zero when any rank failed or fewer than N came up)."""
+    import socket
+    import subprocess
+    with socket.socket() as so:  # a free port for the rendezvous
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % args.gpus, "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL across processes)
+    return subprocess.call(cmd, env=env)
+
+
+class StubDetector:
+    """Test only (--stub): a CPU stand-in with the Detector calls bench.py
+    makes.  Each frame yields a fixed set of records derived from its pixels,
+    so every rank's gather and the merged count are checkable; no timing of
+    it is ever a measurement."""
+
+    def __init__(self, W, H, levels, params):
+        self.W, self.H = W, H
+        self.grid = sum(((W - params.level_len(i)) // 3 + 1) * ((H - params.level_len(i)) // 3 + 1)
+                        for i in range(levels) if params.level_len(i) <= min(W, H))
+        self.rank, self.world, self.t = 0, 1, {}
+
+    def set_options(self, **kw):
+        pass
+
+    def set_shard(self, rank, world):
+        self.rank, self.world = rank, world
+
+    def _records(self, frames):
+        import surfcascade_amd as sc
+        out = []
+        for f in range(frames.shape[0]):
+            v = int(frames[f].sum()) % 7 + 2  # 2..8 records per frame
+            for k in range(v):
+                if k % self.world == self.rank:  # grid sharding: this rank's rows only
+                    out.append((f, k % 3, 3 * k, 3 * k, 70, 70, 10, 0, 0.5 + k / 64))
+        return np.array(out, sc.RECORD_DTYPE)
+
+    def enqueue_device(self, frames, recs, counts):
+        import surfcascade_amd as sc
+        a = self._records(frames.numpy())
+        cap = recs.numel() // sc.RECORD_DTYPE.itemsize
+        k = min(cap, len(a))
+        recs.numpy()[:k * sc.RECORD_DTYPE.itemsize] = a[:k].view(np.uint8)
+        counts.zero_()
+        counts[0] = len(a)
+        for f in range(frames.shape[0]):
+            counts[1 + f] = int((a["frame"] == f).sum())
+        self.t.setdefault("windows", [0.0, 0])[1] += 1
+        self.t["windows"][0] += 1.0
+
+    def synchronize(self):
+        pass
+
+    def info(self, key):
+        return self.grid if key == "grid_windows" else 0
+
+    def set_timing(self, on=True):
+        pass
+
+    def get_timing(self):
+        t, self.t = self.t, {}
+        return {k: tuple(v) for k, v in t.items()} or {"windows": (0.0, 0)}
+
+    def detect_batch(self, frames):
+        return []
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(world_env or "1")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    if world != args.gpus:
+        print("error: --gpus %d but WORLD_SIZE %d: refusing to measure a different GPU count"
+              % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
 
     import torch
     import surfcascade_amd as sc
     from surfcascade_amd import synth
     from surfcascade_amd.dist import enqueue_and_gather, merge_records, shard_range
 
-    torch.cuda.set_device(local_rank)
+    stub = args.stub
+    if stub:
+        dev = torch.device("cpu")
+    else:
+        if torch.cuda.device_count() < world:
+            print("error: %d ranks but %d visible GPUs" % (world, torch.cuda.device_count()),
+                  file=sys.stderr)
+            sys.exit(2)
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if stub:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != args.gpus:
+            print("error: process group of %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus),
+                  file=sys.stderr)
+            sys.exit(2)
+
+    def sync():
+        if not stub:
+            torch.cuda.synchronize()
 
     W, H, B = args.width, args.height, args.batch
     # frame sharding: rank r owns frames 1000 + r*B .. (seeds) -- C3 layout;
@@ -190,10 +301,11 @@ def main():
     grid_shard = args.shard == "grid"
     start = 0 if grid_shard else shard_range(B * world, world, rank)[0]
     host_frames = synth.make_frames(W, H, B, seed0=1000 + start)
-    frames = torch.from_numpy(host_frames).to(f"cuda:{local_rank}")
+    frames = torch.from_numpy(host_frames).to(dev)
     params = (sc.ScanParams.pedestrian(n_levels=args.levels) if args.pedestrian
               else sc.ScanParams(n_levels=args.levels))
-    det = sc.Detector(args.model, params, device=local_rank)
+    det = (StubDetector(W, H, args.levels, params) if stub
+           else sc.Detector(args.model, params, device=local_rank))
     opts = {}
     for o in args.opt:
         k, v = o.split("=", 1)
@@ -203,14 +315,13 @@ def main():
         det.set_shard(rank, world)
     # record buffers: grown (every rank, same size) whenever a scan finds more
     # detections than they hold -- never truncated (dist.enqueue_and_gather)
-    counts = torch.zeros(1 + B, dtype=torch.int32, device=frames.device)
-    state = {"recs": torch.zeros(256 * B * sc.RECORD_DTYPE.itemsize, dtype=torch.uint8,
-                                 device=frames.device)}
+    counts = torch.zeros(1 + B, dtype=torch.int32, device=dev)
+    state = {"recs": torch.zeros(256 * B * sc.RECORD_DTYPE.itemsize, dtype=torch.uint8, device=dev)}
     gathered = {}
 
     def step():
         if dist is not None:  # RCCL gather: counts + capacities, then records padded to the max
-            gc, gr, state["recs"] = enqueue_and_gather(det, frames, state["recs"], counts)
+            gc, gr, state["recs"] = enqueue_and_gather(det, frames, state["recs"], counts, b_max=B)
             gathered["counts"], gathered["recs"] = gc, gr
         else:
             det.enqueue_device(frames, state["recs"], counts)
@@ -219,8 +330,7 @@ def main():
     def check_capacity():  # N = 1: the same frames every step -> checked around the timed loop
         n = int(counts[0].item())
         if n * sc.RECORD_DTYPE.itemsize > state["recs"].numel():
-            state["recs"] = torch.zeros(n * sc.RECORD_DTYPE.itemsize, dtype=torch.uint8,
-                                        device=frames.device)
+            state["recs"] = torch.zeros(n * sc.RECORD_DTYPE.itemsize, dtype=torch.uint8, device=dev)
             step()
         gathered["counts"], gathered["recs"] = [counts.cpu().numpy()], [state["recs"].cpu()]
 
@@ -233,11 +343,11 @@ def main():
     det.set_timing(True)
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
+    sync()
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
@@ -248,10 +358,10 @@ def main():
         check_capacity()
     # single-frame latency (C2 names "1080p frame"): batch-1 steps, device-resident
     lat = None
-    if args.latency_steps > 0 and not grid_shard:
+    if args.latency_steps > 0 and not grid_shard and not stub:
         one = frames[:1]
-        c1 = torch.zeros(2, dtype=torch.int32, device=frames.device)
-        r1 = torch.zeros(1 << 20, dtype=torch.uint8, device=frames.device)
+        c1 = torch.zeros(2, dtype=torch.int32, device=dev)
+        r1 = torch.zeros(1 << 20, dtype=torch.uint8, device=dev)
         for _ in range(3):
             det.enqueue_device(one, r1, c1)
             det.synchronize()
@@ -260,19 +370,23 @@ def main():
             det.enqueue_device(one, r1, c1)
             det.synchronize()
         lat = (time.perf_counter() - t1) / args.latency_steps
+        if int(c1[0].item()) * sc.RECORD_DTYPE.itemsize > r1.numel():  # (never truncates silently)
+            raise RuntimeError("latency leg: %d detections overflow its record buffer" % int(c1[0]))
     # the host-buffer boundary (sc_detect_batch: pageable u8 frames in, raw
     # windows out, H2D + D2H over PCIe inside): reported beside, never `value`
     host_dt = None
-    if args.host_steps > 0 and not grid_shard:
+    if args.host_steps > 0 and not grid_shard and not stub:
         det.detect_batch(host_frames)
         t1 = time.perf_counter()
         for _ in range(args.host_steps):
             det.detect_batch(host_frames)
         host_dt = (time.perf_counter() - t1) / args.host_steps
+    rccl_world = None
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=frames.device)
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+        rccl_world = dist.get_world_size()
     merged = merge_records(gathered["counts"], gathered["recs"],
                            [0 if grid_shard else shard_range(B * world, world, r)[0]
                             for r in range(world)])
@@ -286,22 +400,12 @@ def main():
         tab_bytes = 32 * (W + 1) * (H + 1)
         ms_win, n_win = kt["windows"]
         avg_win_s = ms_win / 1e3 / max(n_win, 1)
-        achieved = tab_bytes * B / avg_win_s / 1e9
+        achieved = tab_bytes * B / max(avg_win_s, 1e-12) / 1e9
         # whole pipeline (SURVEY.md 8d per-unit figure: W*H + 64 (W+1)(H+1) per frame)
         pipe_bytes = W * H + 64 * (W + 1) * (H + 1)
-        pipe_s = sum(v[0] for v in kt.values()) / 1e3 / max(n_win, 1)
-        # PMC per launch of the window kernel for this workload (profiles/pmc_windows.json,
-        # written by profiles/pmc_summary.py from the committed rocprofv3 passes)
-        traffic, valu_insts, pmc_src = None, None, None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_windows.json")
-        if os.path.exists(pmc_path) and not opts:
-            with open(pmc_path) as f:
-                pm = json.load(f)
-            if (pm.get("batch") == B and pm.get("width") == W and pm.get("levels") == args.levels
-                    and pm.get("config", "C2") == args.config):
-                traffic = pm.get("hbm_bytes_per_launch")
-                valu_insts = pm.get("valu_insts_per_launch")
-                pmc_src = pm.get("source")
+        pipe_s = max(sum(v[0] for v in kt.values()) / 1e3 / max(n_win, 1), 1e-12)
+        pmc = pmc_for(args, B, W) if not opts and not stub else {}
+        traffic, valu_insts = pmc.get("hbm_bytes_per_launch"), pmc.get("valu_insts_per_launch")
         line = {
             "metric": CONFIGS[args.config]["metric"],
             "value": value,
@@ -325,26 +429,16 @@ def main():
                        "levels": args.levels,
                        "parallelism": ("grid-row-sharded x%d" if grid_shard else "frame-sharded dp%d")
                        % world},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "cascade_kernel" if opts.get("full_grid") else "chain_kernel",
-                         "avg_launch_ms": avg_win_s * 1e3,
-                         "bytes_per_launch": tab_bytes * B,
-                         "pipeline_achieved": pipe_bytes * B / pipe_s / 1e9,
-                         "pipeline_frac": pipe_bytes * B / pipe_s / 1e9 / HBM_PEAK_GBS,
-                         # beyond-L2 bytes per compulsory byte: re-reads of the table
-                         "traffic_ratio": traffic / (tab_bytes * B) if traffic else None,
-                         # compute side: VALU wave-instructions per launch (PMC
-                         # SQ_INSTS_VALU) over the chip's issue rate (1024 SIMDs x
-                         # 0.5 wave-instr/cycle x 2.4 GHz, MI355X_MICROARCH.md) x
-                         # this launch's time
-                         "valu": (valu_insts / VALU_ISSUE_PEAK / avg_win_s) if valu_insts else None,
-                         "valu_insts_per_launch": valu_insts, "valu_peak_per_s": VALU_ISSUE_PEAK,
-                         "pmc_source": pmc_src},
+            "roofline": roofline(achieved, traffic, valu_insts, avg_win_s, tab_bytes * B, pipe_bytes * B,
+                                 pipe_s, pmc, opts),
             "kernel_ms_per_launch": {k: v[0] / max(v[1], 1) for k, v in kt.items()},
             "visited_windows_last_step": visited,
             "detections_last_step": total_det,
         }
+        if rccl_world is not None:
+            line["process_group"] = {"backend": "gloo" if stub else "nccl (RCCL)", "world_size": rccl_world}
+        if stub:
+            line["stub"] = "CPU stand-in detector (launcher test): not a measurement"
         if lat is not None:
             line["latency_batch1"] = {
                 "ms_per_frame": lat * 1e3, "value": grid / lat, "unit": "windows/s",
@@ -357,7 +451,7 @@ def main():
                 "value": grid * B / host_dt, "unit": "windows/s", "ms_per_step": host_dt * 1e3,
                 "steps": args.host_steps, "per": "GPU",
                 "path": "sc_detect_batch: %d pageable host frames in (H2D), raw windows out (D2H)" % B}
-        if not args.no_cpu and world == 1:
+        if not args.no_cpu and world == 1 and not stub:
             line["cpu_baseline"] = cpu_baseline(host_frames, args.model, args.levels, args.cpu_seconds,
                                                 args.pedestrian)
             line["vs_cpu"] = value / world / line["cpu_baseline"]["value"]
@@ -365,6 +459,53 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def pmc_for(args, B, W):
+    """PMC per launch of the window kernel for this workload (profiles/
+    pmc_windows.json, keyed per config; written by profiles/pmc_summary.py from
+    the committed rocprofv3 passes), or {}."""
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_windows.json")
+    if not os.path.exists(pmc_path):
+        return {}
+    with open(pmc_path) as f:
+        pm = json.load(f)
+    entries = pm.get("configs", {}).values() if "configs" in pm else [pm]
+    for e in entries:
+        if (e.get("batch") == B and e.get("width") == W and e.get("levels") == args.levels
+                and e.get("config", "C2") == args.config):
+            return e
+    return {}
+
+
+def roofline(achieved, traffic, valu_insts, avg_win_s, bytes_launch, pipe_bytes, pipe_s, pmc, opts):
+    r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+         "kernel": "cascade_kernel" if opts.get("full_grid") else "chain_kernel",
+         "avg_launch_ms": avg_win_s * 1e3,
+         "bytes_per_launch": bytes_launch,
+         "pipeline_achieved": pipe_bytes / pipe_s / 1e9,
+         "pipeline_frac": pipe_bytes / pipe_s / 1e9 / HBM_PEAK_GBS,
+         # beyond-L2 bytes per compulsory byte: re-reads of the table
+         "traffic_ratio": traffic / bytes_launch if traffic else None,
+         # compute side: VALU wave-instructions per launch (PMC SQ_INSTS_VALU)
+         # over the chip's issue rate (1024 SIMDs x 0.5 wave-instr/cycle x
+         # 2.4 GHz, MI355X_MICROARCH.md) x this launch's time
+         "valu": (valu_insts / VALU_ISSUE_PEAK / avg_win_s) if valu_insts else None,
+         "valu_insts_per_launch": valu_insts, "valu_peak_per_s": VALU_ISSUE_PEAK,
+         "pmc_source": pmc.get("source")}
+    # the level the kernel actually stresses: L2 misses (128-B lines from the
+    # Infinity Cache / HBM, TCC_MISS) per second over the measured gather
+    # ceiling of the same 16-B-per-lane shape (profiles/calib, k_mall_sparse)
+    miss = pmc.get("counters_per_launch", {}).get("TCC_MISS_sum")
+    ceil = pmc.get("fabric_ceiling_lines_per_s")
+    if miss and ceil:
+        r["fabric_lines_per_s"] = miss / avg_win_s
+        r["fabric_ceiling_lines_per_s"] = ceil
+        r["fabric_frac"] = miss / avg_win_s / ceil
+        hit = pmc["counters_per_launch"].get("TCC_HIT_sum")
+        r["l2_hit"] = hit / (hit + miss) if hit else None
+    return r
 
 
 if __name__ == "__main__":

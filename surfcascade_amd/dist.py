@@ -53,13 +53,34 @@ def _capacity(recs):
     return recs.numel() * recs.element_size() // RECORD_DTYPE.itemsize
 
 
-def _gather_meta(counts, recs, group):
-    """One all_gather of every rank's (counts..., capacity) as int64 ->
-    host array [world, 2 + B]."""
+def _frames_max(counts, group, b_max):
+    """Frames per rank (len(counts) - 1) may differ between ranks (e.g. 257
+    frames over 8 GPUs): the meta all_gather needs one size on every rank, so
+    without a caller-supplied b_max the ranks first all_gather their B."""
+    import torch
+    import torch.distributed as dist
+    b = counts.numel() - 1
+    if b_max is not None:
+        if b > b_max:
+            raise ValueError("rank has %d frames, b_max %d" % (b, b_max))
+        return b_max
+    world = dist.get_world_size(group)
+    mine = torch.tensor([b], dtype=torch.int64, device=counts.device)
+    bs = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(bs, mine, group=group)
+    return int(max(int(x.item()) for x in bs))
+
+
+def _gather_meta(counts, recs, group, b_max=None):
+    """One all_gather of every rank's (B, counts padded to b_max frames,
+    capacity) as int64 -> host array [world, 3 + b_max]."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
-    meta = torch.cat([counts.to(torch.int64).reshape(-1),
+    bm = _frames_max(counts, group, b_max)
+    c = counts.to(torch.int64).reshape(-1)
+    pad = torch.zeros(1 + bm - c.numel(), dtype=torch.int64, device=counts.device)
+    meta = torch.cat([torch.tensor([c.numel() - 1], dtype=torch.int64, device=counts.device), c, pad,
                       torch.tensor([_capacity(recs)], dtype=torch.int64, device=counts.device)])
     gm = [torch.zeros_like(meta) for _ in range(world)]
     dist.all_gather(gm, meta, group=group)
@@ -69,7 +90,7 @@ def _gather_meta(counts, recs, group):
 def _gather_records(gm, counts, recs, group):
     import torch
     import torch.distributed as dist
-    ns = [int(m[0]) for m in gm]
+    ns = [int(m[1]) for m in gm]
     for r, m in enumerate(gm):
         if ns[r] > int(m[-1]):
             raise RecordOverflow(r, ns[r], int(m[-1]))
@@ -80,22 +101,25 @@ def _gather_records(gm, counts, recs, group):
         if send.numel() < nb:  # a smaller buffer than another rank's count: pad (sizes must match)
             send = torch.cat([send, torch.zeros(nb - send.numel(), dtype=recs.dtype, device=recs.device)])
         dist.all_gather(gr, send.contiguous(), group=group)
-    gc = [m[:-1].astype(np.int32) for m in gm]
+    # each rank's own counts: [total, frame 0 .. B_r - 1]
+    gc = [m[1:2 + int(m[0])].astype(np.int32) for m in gm]
     return gc, gr
 
 
-def gather_detections(counts, recs, group=None):
+def gather_detections(counts, recs, group=None, b_max=None):
     """counts: int32 [1+B] (counts[0] = this rank's total), recs: uint8
-    [cap*40] record buffer (sc_enqueue_device's outputs, same B on every rank).
+    [cap*40] record buffer (sc_enqueue_device's outputs).  B may differ
+    between ranks; b_max (the largest B, when the caller knows it) saves the
+    size exchange.
 
     1) all_gather of the counts (and capacities); 2) all_gather of every
     rank's first max(count) records (padded).  Raises RecordOverflow on every
     rank when any rank's count exceeds its capacity (its buffer lost records).
     Returns (per-rank counts, per-rank record bytes)."""
-    return _gather_records(_gather_meta(counts, recs, group), counts, recs, group)
+    return _gather_records(_gather_meta(counts, recs, group, b_max), counts, recs, group)
 
 
-def enqueue_and_gather(det, frames, recs, counts, group=None):
+def enqueue_and_gather(det, frames, recs, counts, group=None, b_max=None):
     """One detect step of a rank followed by the gather: scans `frames` into
     `recs` / `counts` (sc_enqueue_device); when some rank's detections
     overflowed its buffer, every rank grows its buffer to the largest count
@@ -103,14 +127,14 @@ def enqueue_and_gather(det, frames, recs, counts, group=None):
     import torch
     det.enqueue_device(frames, recs, counts)
     det.synchronize()
-    gm = _gather_meta(counts, recs, group)
-    need = int(gm[:, 0].max())
-    if (gm[:, 0] > gm[:, -1]).any():
+    gm = _gather_meta(counts, recs, group, b_max)
+    need = int(gm[:, 1].max())
+    if (gm[:, 1] > gm[:, -1]).any():
         if need > _capacity(recs):
             recs = torch.zeros(need * RECORD_DTYPE.itemsize, dtype=torch.uint8, device=recs.device)
         det.enqueue_device(frames, recs, counts)
         det.synchronize()
-        gm = _gather_meta(counts, recs, group)
+        gm = _gather_meta(counts, recs, group, b_max)
     gc, gr = _gather_records(gm, counts, recs, group)
     return gc, gr, recs
 

@@ -25,7 +25,7 @@ def _records_for(oracle, casc, frames, params, frame0, rng):
     return a
 
 
-def _worker(rank, world, port, n_frames, out_q, tight=False):
+def _worker(rank, world, port, n_frames, out_q, tight=False, own_b=False):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -44,7 +44,9 @@ def _worker(rank, world, port, n_frames, out_q, tight=False):
     cap = len(a) if tight else 1 << 15
     buf = np.zeros(cap, RECORD_DTYPE)
     buf[:len(a)] = a
-    B = max(shard_range(n_frames, world, r)[1] for r in range(world))
+    # own_b: each rank's counts hold its own frames only (uneven shards: 5
+    # frames over 2 ranks -> 3 and 2; the gather exchanges the sizes first)
+    B = cnt if own_b else max(shard_range(n_frames, world, r)[1] for r in range(world))
     counts = np.zeros(1 + B, np.int32)
     counts[0] = len(a)
     for f in range(cnt):
@@ -68,15 +70,16 @@ def test_shard_range_covers_all():
         assert seen == list(range(n))
 
 
-@pytest.mark.parametrize("world,tight", [(2, False), (2, True)])
-def test_gloo_gather_equals_single_process(oracle, world, tight):
+@pytest.mark.parametrize("world,tight,own_b", [(2, False, False), (2, True, False), (2, False, True)])
+def test_gloo_gather_equals_single_process(oracle, world, tight, own_b):
     from surfcascade_amd import RECORD_DTYPE, synth
     from surfcascade_amd.dist import merge_records
     n_frames = 5
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + os.getpid() % 1000 + (7 if tight else 0)
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_frames, q, tight)) for r in range(world)]
+    port = 29500 + os.getpid() % 1000 + (7 if tight else 0) + (13 if own_b else 0)
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_frames, q, tight, own_b))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = np.frombuffer(q.get(timeout=120), RECORD_DTYPE)
