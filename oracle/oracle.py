@@ -103,6 +103,9 @@ def lib():
         L.sco_detect_frame.restype = ctypes.c_int64
         L.sco_exposure.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ScoModel),
                                    ctypes.POINTER(ScoParams), _i64p, ctypes.c_int]
+        L.sco_exp_sensitivity.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ScoModel),
+                                          ctypes.POINTER(ScoParams), _i64p, ctypes.c_void_p,
+                                          ctypes.c_int64, ctypes.c_int]
         L.sco_walk_grid.argtypes = [_i16p, _f32p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_double, _u8p]
         L.sco_walk_grid.restype = ctypes.c_int64
@@ -422,6 +425,18 @@ def exposure(T, cascade: Cascade, params: Params, nthreads=None):
     lib().sco_exposure(_p(T, _f32p), W, H, ctypes.byref(m), ctypes.byref(params.c()), _p(st, _i64p),
                        _nt(nthreads))
     return st
+
+
+def exp_sensitivity(T, cascade: Cascade, params: Params, zcap=4096, nthreads=None):
+    """sco_exp_sensitivity counters (see sc_oracle.c) for one frame's table
+    -> (int64[9], z values of the flipping evaluations)."""
+    H, W = T.shape[0] - 1, T.shape[1] - 1
+    st = np.zeros(9, np.int64)
+    zd = np.zeros(zcap, np.float64)
+    m = cascade.c()
+    lib().sco_exp_sensitivity(_p(T, _f32p), W, H, ctypes.byref(m), ctypes.byref(params.c()),
+                              _p(st, _i64p), zd.ctypes.data, zcap, _nt(nthreads))
+    return st, zd[:min(int(st[1]), zcap)]
 
 
 def walk_grid(p_grid, s_grid, layout, n_stages, stride_score=0.5):

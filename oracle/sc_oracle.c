@@ -499,6 +499,197 @@ void sco_exposure(const float *T, int W, int H, const sco_model *m, const sco_pa
     st[0] = a0; st[1] = a1; st[2] = a2; st[3] = a3; st[4] = a4; st[5] = a5; st[6] = a6; st[7] = a7;
 }
 
+/* ---- exp() sensitivity, exact (VERDICT r2 Next 6) ----------
+ * The reference's sigmoid calls the MSVC CRT exp (LogisticRegression.cpp:65),
+ * which is not in /root/reference.  Model: the CRT result e' lies within one
+ * f64 ulp of glibc's e = exp(-z) (both are faithful; glibc's is correctly
+ * rounded on these arguments, checked with mpmath by profiles/exposure.py).
+ * Over the windows the reference visits (the sco_detect chain), every weak
+ * evaluation is recomputed with e' = nextafter(e, -inf) and nextafter(e, +inf)
+ * through the reference's f64 ops, 1.0/(1.0 + e'), cast to float.  A weak
+ * "flips" when such an alternative f32 differs from the baseline.  For every
+ * flipping alternative the window is re-evaluated with that one weak output
+ * replaced, and when the window's result (p, s_last) changes, the row's x
+ * chain is re-walked from it until it rejoins the baseline chain; detections
+ * that appear or vanish on the way are counted.
+ *  st[0] weak evaluations             st[1] evaluations with a flipping alternative
+ *  st[2] flipping alternatives        st[3] alternatives that flip a stage decision
+ *  st[4] alternatives that change the window's (p, s_last) bits
+ *  st[5] alternatives that change the window's stride (good / skip)
+ *  st[6] detections that appear or vanish (window itself + chain re-walk)
+ *  st[7] windows with two or more flipping evaluations
+ *  st[8] alternatives that leave a detection a detection with other score
+ *        bits (a 1-ulp change of s_last: ~1e-8 on (s + S + 1)/S, inside
+ *        north_star's 1e-5 score tolerance)
+ * zd: the z of the first zcap flipping evaluations (for the mpmath check). */
+static float lr_alt(const float *w, double bias, const float f[32], float *alt_lo, float *alt_hi,
+                    double *z_out) {
+    float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int i = 0; i < 32; i += 4)
+        for (int j = 0; j < 4; j++) s[j] = w[i + j] * f[i + j] + s[j];
+    float z32 = (s[0] + s[1]) + (s[2] + s[3]);
+    double z = (double)z32;
+    z += (double)w[32] * bias;
+    double e = exp(-z);
+    *z_out = z;
+    *alt_lo = (float)(1.0 / (1.0 + nextafter(e, -INFINITY)));
+    *alt_hi = (float)(1.0 / (1.0 + nextafter(e, INFINITY)));
+    return (float)(1.0 / (1.0 + e));
+}
+
+/* sco_eval_window with weak g's output replaced by v (g < 0: none). */
+static int eval_window_ovr(const float *T, int W, const sco_model *m, int l, int lh, int x, int y,
+                           float k, float *s_last, int64_t g, float v) {
+    if (!sco_prefilter(T, W, x, y, l, lh, k, NULL)) return -1;
+    float scale = (float)l / (float)m->tmpl_w;
+    int p;
+    float score = 0.0f;
+    int64_t off = 0;
+    for (p = 0; p < m->n_stages; p++) {
+        float sum = 0.0f;
+        for (int q = 0; q < m->n_weak[p]; q++) {
+            if (off + q == g) {
+                sum += v;
+                continue;
+            }
+            int32_t pr[4];
+            float f[32];
+            sco_project(m->patch + 4 * (off + q), scale, x, y, pr);
+            sco_calc_feature(T, W, pr, f);
+            sum += sco_lr_predict(m->w + 33 * (off + q), m->bias[off + q], f);
+        }
+        score = sum / (float)m->n_weak[p];
+        off += m->n_weak[p];
+        if ((double)score < (double)m->theta[p]) break;
+    }
+    *s_last = score;
+    return p;
+}
+
+void sco_exp_sensitivity(const float *T, int W, int H, const sco_model *m, const sco_params *p,
+                         int64_t st[9], double *zd, int64_t zcap, int nthreads) {
+    int stp = sco_step(p), nl = sco_effective_levels(W, H, p);
+    const int S = m->n_stages;
+    int64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0, a8 = 0, nz = 0;
+#pragma omp parallel for schedule(dynamic) num_threads(nthreads > 0 ? nthreads : 1) \
+    reduction(+ : a0, a1, a2, a3, a4, a5, a6, a7, a8)
+    for (int i = 0; i < nl; i++) {
+        int l = sco_level_len(p->base_len, i), lh = l * p->aspect_h;
+        if (l > W || lh > H) continue;
+        int nx = (W - l) / stp + 1;
+        float scale = (float)l / (float)m->tmpl_w;
+        /* per row: baseline results of the visited windows (-3: not visited) */
+        int *bp = (int *)malloc(sizeof(int) * nx);
+        float *bs = (float *)malloc(sizeof(float) * nx);
+        /* flips of the row: (window, weak, alternative value) */
+        int64_t fcap = 64, nf = 0;
+        int64_t *fw = (int64_t *)malloc(sizeof(int64_t) * 2 * fcap);
+        float *fv = (float *)malloc(sizeof(float) * fcap);
+        for (int y = 0; y <= H - lh; y += stp) {
+            for (int j = 0; j < nx; j++) bp[j] = -3;
+            nf = 0;
+            int multi = 1;
+            for (int j = 0; j < nx; j += multi) {
+                int x = j * stp;
+                if (!sco_prefilter(T, W, x, y, l, lh, p->prefilter_k, NULL)) {
+                    bp[j] = -1;
+                    bs[j] = 0.0f;
+                    multi = 2;
+                    continue;
+                }
+                int pr, nflip = 0;
+                float score = 0.0f;
+                int64_t off = 0;
+                for (pr = 0; pr < S; pr++) {
+                    float sum = 0.0f;
+                    for (int q = 0; q < m->n_weak[pr]; q++) {
+                        int32_t rc[4];
+                        float f[32], lo, hi;
+                        double z;
+                        sco_project(m->patch + 4 * (off + q), scale, x, y, rc);
+                        sco_calc_feature(T, W, rc, f);
+                        float v = lr_alt(m->w + 33 * (off + q), m->bias[off + q], f, &lo, &hi, &z);
+                        a0++;
+                        if (lo != v || hi != v) {
+                            a1++;
+                            nflip++;
+#pragma omp critical(sco_zd)
+                            {
+                                if (zd && nz < zcap) zd[nz] = z;
+                                nz++;
+                            }
+                            float alts[2] = {lo, hi};
+                            for (int u = 0; u < 2; u++) {
+                                if (alts[u] == v || (u == 1 && alts[1] == alts[0])) continue;
+                                if (nf == fcap) {
+                                    fcap *= 2;
+                                    fw = (int64_t *)realloc(fw, sizeof(int64_t) * 2 * fcap);
+                                    fv = (float *)realloc(fv, sizeof(float) * fcap);
+                                }
+                                fw[2 * nf] = j;
+                                fw[2 * nf + 1] = off + q;
+                                fv[nf++] = alts[u];
+                            }
+                        }
+                        sum += v;
+                    }
+                    score = sum / (float)m->n_weak[pr];
+                    off += m->n_weak[pr];
+                    if ((double)score < (double)m->theta[pr]) break;
+                }
+                a7 += nflip >= 2;
+                bp[j] = pr;
+                bs[j] = score;
+                multi = final_score(score, pr, S) < p->stride_score ? 2 : 1;
+            }
+            /* every flipping alternative of the row, one at a time */
+            for (int64_t t = 0; t < nf; t++) {
+                const int j = (int)fw[2 * t];
+                const int64_t g = fw[2 * t + 1];
+                a2++;
+                float s2;
+                int p2 = eval_window_ovr(T, W, m, l, lh, j * stp, y, p->prefilter_k, &s2, g, fv[t]);
+                if (p2 == bp[j] && s2 == bs[j]) continue;
+                a4++;
+                /* the stage decision that flipped: the first stage where they part */
+                a3 += p2 != bp[j];
+                const int good0 = !(final_score(bs[j], bp[j], S) < p->stride_score);
+                const int good2 = !(final_score(s2, p2, S) < p->stride_score);
+                const int det0 = bp[j] == S, det2 = p2 == S;
+                a6 += det0 != det2;
+                a8 += det0 && det2 && s2 != bs[j];
+                if (good0 == good2) continue;
+                a5++;
+                /* re-walk the chain from j with the alternative until it lands
+                 * on a window the baseline chain visits (identical after that) */
+                int k2 = j + (good2 ? 1 : 2);
+                int kb = j + (good0 ? 1 : 2);  /* baseline chain's next visit */
+                while (k2 < nx) {
+                    while (kb < k2 && kb < nx) {  /* baseline windows skipped by the new chain */
+                        if (bp[kb] == S) a6++;
+                        kb += (bp[kb] < 0 || final_score(bs[kb], bp[kb], S) < p->stride_score) ? 2 : 1;
+                    }
+                    if (kb == k2) break;  /* rejoined */
+                    float s3;
+                    int p3 = eval_window_ovr(T, W, m, l, lh, k2 * stp, y, p->prefilter_k, &s3, -1, 0.0f);
+                    if (p3 == S) a6++;    /* a window only the new chain visits */
+                    k2 += (p3 < 0 || final_score(s3, p3, S) < p->stride_score) ? 2 : 1;
+                }
+                while (k2 >= nx && kb < nx) {  /* the new chain left the row first */
+                    if (bp[kb] == S) a6++;
+                    kb += (bp[kb] < 0 || final_score(bs[kb], bp[kb], S) < p->stride_score) ? 2 : 1;
+                }
+            }
+        }
+        free(bp);
+        free(bs);
+        free(fw);
+        free(fv);
+    }
+    st[0] = a0; st[1] = a1; st[2] = a2; st[3] = a3; st[4] = a4; st[5] = a5; st[6] = a6; st[7] = a7;
+    st[8] = a8;
+}
+
 /* In-memory u8 frame -> raw detections (the reference's per-image body,
  * ObjDetector.cpp:165-220, without decode / file I/O). */
 int64_t sco_detect_frame(const uint8_t *img, int W, int H, int stride,

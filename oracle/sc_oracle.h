@@ -91,6 +91,10 @@ int64_t sco_walk_grid(const int16_t *p_grid, const float *s_grid, const int64_t 
                       int n_levels, int n_stages, double stride_score, uint8_t *visited);
 void sco_exposure(const float *T, int W, int H, const sco_model *m, const sco_params *p,
                   int64_t st[8], int nthreads);
+/* exp() sensitivity of the visited windows (VERDICT r2 Next 6): counters in
+ * sc_oracle.c; zd receives the z of the first zcap flipping evaluations. */
+void sco_exp_sensitivity(const float *T, int W, int H, const sco_model *m, const sco_params *p,
+                         int64_t st[9], double *zd, int64_t zcap, int nthreads);
 int64_t sco_detect_frame(const uint8_t *img, int W, int H, int stride,
                          const sco_model *m, const sco_params *p,
                          sco_window *out, int64_t cap, int64_t *n_visited,
