@@ -192,9 +192,12 @@ int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, 
 int sc_detector_info(sc_detector *d, int what, int64_t *value);
 
 /* ---- tuning and test options ---------------------------------------------
- * Schedule / layout choices that never change a result bit (the parity tests
- * run every one of them); the defaults are the measured-fastest.  The library
- * reads no environment variable: these are set per detector, explicitly. */
+ * Options 1-14 and 17 are schedule / layout choices that never change a result bit
+ * (tests/test_gpu_parity.py runs each against the oracle); the defaults are
+ * the measured-fastest.  Options 15-16 restrict the scan to a range of levels
+ * (profiling of level groups): they DO change the result, to the windows of
+ * those levels.  The library reads no environment variable: these are set per
+ * detector, explicitly. */
 #define SC_OPT_FULL_GRID 1    /* 1: evaluate every grid window (cascade + walk   */
                               /* kernels) instead of the lazy chain kernel (0) */
 #define SC_OPT_CHUNK_MIN 2    /* stages with >= this many survivors run one lane */
@@ -217,6 +220,11 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
                               /* one-frame launch, else 8; or 1, 2, 4, 8)      */
 #define SC_OPT_INTEGRAL_PASSES 14 /* integral: 0 auto (two passes up to 3     */
                               /* frames), 1 colstrip, 2 rowfull + colsum       */
+#define SC_OPT_LEVEL_LO 15    /* scan only levels >= LEVEL_LO (default 0)      */
+#define SC_OPT_LEVEL_HI 16    /* ... and < LEVEL_HI (0: every level)           */
+#define SC_OPT_CHAIN_WAVES 17 /* chain kernel waves per CU: 0 auto (16 when the  */
+                              /* model and their scratch fit the LDS and a     */
+                              /* frame's table is <= 128 MiB), 12, 16          */
 int sc_detector_set_option(sc_detector *d, int option, int64_t value);
 
 /* Enable per-window debug records (grid order) for the next detect calls. */

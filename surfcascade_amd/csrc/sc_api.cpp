@@ -126,6 +126,8 @@ struct sc_detector {
         int full_grid = 0, chunk_min = 0, table_layout = 0, phases = 0, substrips = 0;
         int band_rows = 0, row_order = 2, row_block = 32, chain_chunk = 0;
         int lds_weights = -1, wgs_per_cu = 0, profile = 0, chain_segs = 0, integral_passes = 0;
+        int level_lo = 0, level_hi = 0;  // scan only levels [lo, hi) (hi 0: all)
+        int chain_waves = 0;             // chain kernel waves per workgroup (0 auto)
     } opt;
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
@@ -284,7 +286,9 @@ void build_geometry(sc_detector *d, int W, int H) {
             L.pre_row = L.lh * tg.rowp;
             if (L.nx > 4096)  // walk kernel: one wave, 64 chunks of 64 windows per row
                 throw Error{SC_ERR_INVALID, "more than 4096 windows per row (frame too wide)"};
-            for (int r = 0; r < L.ny; r++) ng.rows.push_back(make_int2(i, r * ng.step));
+            const bool scanned = i >= d->opt.level_lo && (d->opt.level_hi == 0 || i < d->opt.level_hi);
+            if (scanned)  // SC_OPT_LEVEL_LO / _HI (level-group profiling); grid indices stay the frame's
+                for (int r = 0; r < L.ny; r++) ng.rows.push_back(make_int2(i, r * ng.step));
             gb += (long long)L.nx * L.ny;
             ng.nx_max = std::max(ng.nx_max, L.nx);
         }
@@ -561,7 +565,7 @@ void ensure_buffers(sc_detector *d, int n) {
 }
 
 sc::LaunchCfg launch_cfg(const sc_detector *d) {
-    return sc::LaunchCfg{d->cus, d->opt.lds_weights, d->opt.wgs_per_cu};
+    return sc::LaunchCfg{d->cus, d->opt.lds_weights, d->opt.wgs_per_cu, d->opt.chain_waves};
 }
 
 void timed_begin(sc_detector *d, hipEvent_t *a) {
@@ -856,30 +860,53 @@ int mine_sync(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int 
     HIPCHK(hipGetLastError());
     sc::launch_mine_scatter(ma, d->stream);
     HIPCHK(hipGetLastError());
-    // descriptors of every kept window: kept = min(total, capacity) is only
-    // known on the device, so the feature kernel covers `capacity` windows
-    // and its threads past the total exit (they read the scan's total)
+    // descriptors of every kept window, kept = min(total, capacity).  Host
+    // output: read the scan's total first (the call ends in a host sync
+    // anyway) and size the descriptor buffer and launch to the kept windows
+    // -- a trainer-style capacity (FillNegSamples' n_total) far above the
+    // candidates found then costs nothing.  Device output: kept is only known
+    // on the device, so the feature kernel covers `capacity` windows and its
+    // threads past the device-side total exit (no host round trip).
     const int P = (int)d->all_rects.size() / 4;
-    if (feat && capacity > 0) {
-        if (!feat_device) d->d_feat.ensure((size_t)capacity * P * 32);
+    std::vector<int> fc((size_t)n + 1);
+    auto read_counts = [&] {
+        HIPCHK(hipMemcpyAsync(fc.data(), d->d_mine_fc.p, sizeof(int) * (n + 1), hipMemcpyDeviceToHost,
+                              d->stream));
+        HIPCHK(hipStreamSynchronize(d->stream));
+    };
+    long long total = -1;
+    auto launch_desc = [&](int n_win, float *out) {
         sc::FeatureArgs fa{};
         fa.table = d->d_table.p;
         fa.g = g.tg;
         fa.windows = d->d_mine_win.p;
-        fa.n_windows = capacity;
+        fa.n_windows = n_win;
         fa.n_valid = d->d_mine_fc.p;
         fa.n_patches = P;
         fa.proj_all = d->d_proj_all.p;
-        fa.out = feat_device ? feat : d->d_feat.p;
+        fa.out = out;
         sc::launch_features(fa, d->stream);
         HIPCHK(hipGetLastError());
+    };
+    if (feat && capacity > 0 && feat_device) {
+        launch_desc(capacity, feat);
+    } else if (feat && capacity > 0) {
+        read_counts();
+        total = 0;
+        for (int f = 0; f < n; f++) total += fc[1 + f];
+        const int kept0 = (int)std::min<long long>(total, capacity);
+        if (kept0 > 0) {
+            d->d_feat.ensure((size_t)kept0 * P * 32);
+            launch_desc(kept0, d->d_feat.p);
+        }
     }
-    std::vector<int> fc((size_t)n + 1);
-    HIPCHK(hipMemcpyAsync(fc.data(), d->d_mine_fc.p, sizeof(int) * (n + 1), hipMemcpyDeviceToHost, d->stream));
-    HIPCHK(hipStreamSynchronize(d->stream));
-    long long total = 0;
-    for (int f = 0; f < n; f++) total += fc[1 + f];
+    if (total < 0) {
+        read_counts();
+        total = 0;
+        for (int f = 0; f < n; f++) total += fc[1 + f];
+    }
     const int kept = (int)std::min<long long>(total, capacity);
+    HIPCHK(hipStreamSynchronize(d->stream));  // the descriptor kernel (the copies below are synchronous)
     if (feat && kept > 0 && !feat_device)
         HIPCHK(hipMemcpy(feat, d->d_feat.p, sizeof(float) * (size_t)kept * P * 32, hipMemcpyDeviceToHost));
     std::vector<sc::MineWindow> mw(kept);
@@ -1341,6 +1368,14 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
             case SC_OPT_WGS_PER_CU: o.wgs_per_cu = range(0, 4); regeo = false; break;
             case SC_OPT_PROFILE: o.profile = range(0, 1); regeo = false; break;
             case SC_OPT_INTEGRAL_PASSES: o.integral_passes = range(0, 2); regeo = false; break;
+            case SC_OPT_CHAIN_WAVES:
+                o.chain_waves = range(0, 16);
+                if (o.chain_waves != 0 && o.chain_waves != 12 && o.chain_waves != 16)
+                    throw Error{SC_ERR_INVALID, "chain_waves: 0, 12 or 16"};
+                regeo = false;
+                break;
+            case SC_OPT_LEVEL_LO: o.level_lo = range(0, 256); break;
+            case SC_OPT_LEVEL_HI: o.level_hi = range(0, 256); break;
             case SC_OPT_CHAIN_SEGS:
                 o.chain_segs = range(0, sc::kXcds);
                 if (o.chain_segs & (o.chain_segs - 1)) throw Error{SC_ERR_INVALID, "chain_segs: 0, 1, 2, 4 or 8"};

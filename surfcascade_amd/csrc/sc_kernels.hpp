@@ -233,6 +233,7 @@ struct LaunchCfg {
     int cus;
     int lds_weights;  // -1 auto, 0 off, 1 on (when the model fits)
     int wgs_per_cu;   // 0: occupancy limit
+    int chain_waves;  // chain kernel waves per workgroup: 0 auto (16 when the LDS holds them), 12, 16
 };
 
 // returns the number of workgroups launched

@@ -43,12 +43,6 @@ namespace {
 #define SC_CASCADE_MIN_WGS 1
 #endif
 
-#ifndef SC_CHAIN_WAVES  // chain kernel: waves per workgroup (the model is staged once per workgroup:
-#define SC_CHAIN_WAVES 12  // one 12-wave workgroup per CU leaves the LDS room for 128-window batches)
-#endif
-#ifndef SC_CHAIN_MIN_WGS  // chain kernel: 12 waves per CU
-#define SC_CHAIN_MIN_WGS (12 / SC_CHAIN_WAVES)
-#endif
 
 #ifndef SC_ABL_NOWAIT  // timing ablation only: segments start without the hand-off (wrong results)
 #define SC_ABL_NOWAIT 0
@@ -62,11 +56,34 @@ constexpr int kWavesPerWg = 4;
 constexpr int kItemBuf = SC_ITEM_BUF;
 constexpr int kWalkMaxChunks = 64;  // windows per row <= 4096 (host check)
 constexpr int kCascadeThreads = 64 * kWavesPerWg;
-constexpr int kChainWaves = SC_CHAIN_WAVES;
-constexpr int kChainThreads = 64 * kChainWaves;
+// chain kernel: one workgroup of NW waves per CU (the model is staged in LDS
+// once per workgroup): 16 (4 per SIMD, 128 VGPRs) or 12 (3 per SIMD), chosen
+// per launch (launch_chain).
+
 
 __device__ __forceinline__ unsigned long long lanes_below() {
     return (1ull << (threadIdx.x & 63)) - 1ull;
+}
+
+// This lane's index.  RM: recomputed at each use (v_mbcnt, no input
+// register) and opaque to the optimiser, so per-lane LDS addresses derived
+// from it are rematerialised where they are used instead of being hoisted out
+// of the persistent loop and held in VGPRs for the kernel's whole life: the
+// chain kernel then fits 128 VGPRs (16 waves per CU; 156 -> 134 VGPRs at 12).
+template <bool RM>
+__device__ __forceinline__ int lane_id() {
+    if constexpr (RM) {
+        int l = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        asm volatile("" : "+v"(l));
+        return l;
+    } else {
+        return threadIdx.x & 63;
+    }
+}
+
+// popcount of the bits of m below this lane (v_mbcnt: no 64-bit lane mask held)
+__device__ __forceinline__ int popc_below(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
 // Orders LDS traffic between the lanes of ONE wave (a wave's DS instructions
@@ -219,11 +236,11 @@ struct ItemStats {
     }
 };
 
-template <bool LW, class Rows, class Need, class Stats = NoStats>
+template <bool LW, bool RM, class Rows, class Need, class Stats = NoStats>
 __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B, const char *Tb,
                                              const float4 *Wl, const double *Bl, const int16_t *Ol,
                                              float *P, float *st_s, unsigned *surv, int8_t *st_p,
-                                             int lane, Need need, Stats &&stats = Stats{}) {
+                                             int /*lane*/, Need need, Stats &&stats = Stats{}) {
     const int half_off = a.g.hs, stride = B.stride();
     const float4 *T = reinterpret_cast<const float4 *>(Tb);
     auto cell = [&](unsigned sv) { return B.origin((int)(sv >> 16), (int)(sv & 0xffffu)); };
@@ -237,7 +254,7 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
         const int nw = B.width(r), pre_row = B.pre_row_of(r);
         const float thr = B.thr_of(r);
         for (int b = 0; b < nw; b += 64) {
-            const int u = b + lane;
+            const int u = b + lane_id<RM>();
             bool pass = false;
             if (u < nw && need(r * stride + u)) {
                 const int pre_col = B.pre_col_of(r, u);
@@ -249,7 +266,7 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
                 st_s[r * stride + u] = 0.0f;
             }
             const unsigned long long mk = __ballot(pass);
-            if (pass) surv[nsurv + __popcll(mk & lanes_below())] = ((unsigned)r << 16) | (unsigned)u;
+            if (pass) surv[nsurv + popc_below(mk)] = ((unsigned)r << 16) | (unsigned)u;
             nsurv += __popcll(mk);
             if constexpr (std::remove_reference_t<Stats>::on)
                 stats.pre(__popcll(__ballot(u < nw && need(r * stride + u))), __popcll(mk));
@@ -278,7 +295,7 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
             }
             const unsigned long long mk = __ballot(keep);
             wave_sync();
-            if (keep) surv[nn + __popcll(mk & lanes_below())] = sv;
+            if (keep) surv[nn + popc_below(mk)] = sv;
             nn += __popcll(mk);
             wave_sync();
         };
@@ -286,7 +303,7 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
             // one lane per survivor, k wave-uniform: parameters via scalar loads
             for (int c = 0; c < nsurv; c += 64) {
                 stats.iter(min(64, nsurv - c));
-                const int i = c + lane;
+                const int i = c + lane_id<RM>();
                 unsigned sv = 0;
                 float sum = 0.0f;
                 if (i < nsurv) {
@@ -318,7 +335,7 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
                     k = Ol[off + kk];
                 };
                 for (int b2 = 0; b2 < items; b2 += 64) stats.iter(min(64, items - b2));
-                for (int t2 = lane; t2 < items; t2 += 64) {
+                for (int t2 = lane_id<RM>(); t2 < items; t2 += 64) {
                     int k, i;
                     decode(t2, k, i);
                     const int gk = off + k;
@@ -331,11 +348,12 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
                 wave_sync();
                 unsigned sv = 0;
                 float acc = 0.0f;  // GentleAdaboost.cpp:255-258 order
-                if (lane < G) {
-                    sv = surv[c + lane];
-                    for (int k = 0; k < n; k++) acc += P[k * G + lane];
+                const int ln = lane_id<RM>();
+                if (ln < G) {
+                    sv = surv[c + ln];
+                    for (int k = 0; k < n; k++) acc += P[k * G + ln];
                 }
-                decide(lane < G, sv, acc);
+                decide(ln < G, sv, acc);
             }
         }
         nsurv = nn;
@@ -425,7 +443,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
             const BandRows B{(unsigned)D.t_off, D.nw, D.nr, g.step * g.rowp, D.j0, a.K, D.thr,
                              D.pre_row, D.pre_col[0], D.pre_col[1],
                              a.proj + (long long)D.level * 2 * a.K, g};
-            eval_windows<LW>(a, B, Tb, Wl, Bl, Ol, P, st_s, surv, st_p, lane,
+            eval_windows<LW, false>(a, B, Tb, Wl, Bl, Ol, P, st_s, surv, st_p, lane,
                              [](int) { return true; });
             // 3) per-window results to HBM (coalesced per row)
             const long long gi = (long long)frame * a.grid_per_frame + D.g_off;
@@ -602,11 +620,12 @@ __host__ __device__ inline size_t chain_wave_bytes(int seg_max) {
 // evaluates ~55 % of the grid's weak items (the visited windows alone are
 // 53 %).  Visited windows that
 // passed every stage are emitted with score (s + S + 1)/S (:201-212).
-template <bool LW>
-__global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(CascadeArgs a,
-                                                                                  WalkArgs w) {
+template <bool LW, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkArgs w) {
+    constexpr int kChainWaves = NW, kChainThreads = 64 * NW;
+    constexpr bool RM = NW > 12;  // rematerialised lane values (128-VGPR budget)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: per-wave LDS bases in SGPRs)
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (uniform: per-wave LDS bases in SGPRs)
     float4 *Wl;
     double *Bl;
     int16_t *Ol;
@@ -678,7 +697,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
             pre--;
             const int q0 = q & ((1 << sh) - 1);  // an XCD of segment 0
             int v = 0;
-            if (lane == 0) v = atomicAdd(&a.queues[(q0 * kSubQ + u) * kQueueStride], 1);
+            if (lane_id<RM>() == 0) v = atomicAdd(&a.queues[(q0 * kSubQ + u) * kQueueStride], 1);
             v = ((__builtin_amdgcn_readfirstlane(v) * kSubQ + u) << sh) + q0;
             if (v < n_tasks) {
                 t = v;
@@ -690,7 +709,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
         }
         while (!drained) {
             int v = 0;
-            if (lane == 0) v = atomicAdd(&a.queues[(q * kSubQ + u) * kQueueStride], 1);
+            if (lane_id<RM>() == 0) v = atomicAdd(&a.queues[(q * kSubQ + u) * kQueueStride], 1);
             v = ((__builtin_amdgcn_readfirstlane(v) * kSubQ + u) << sh) + (q & ((1 << sh) - 1));
             if (v < n_tasks) {
                 t = v;
@@ -709,7 +728,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
     };
     // the chain leaves slot sl's segment at absolute position pos: hand it on
     auto finish = [&](int sl, int pos) {
-        if (lane == 0) {
+        if (lane_id<RM>() == 0) {
             if (tq[sl] + 1 < nsg)
                 __hip_atomic_store(&w.entry[(long long)tt[sl] * nsg + tq[sl] + 1], pos + 1,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -723,7 +742,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
             finish(sl, pos);
             return;
         }
-        for (int i = lane; i < 3 * nwords; i += 64) bits0[sl * 3 * nwords + i] = 0ull;
+        for (int i = lane_id<RM>(); i < 3 * nwords; i += 64) bits0[sl * 3 * nwords + i] = 0ull;
         r[sl] = rel;
         st[sl] = 2;
     };
@@ -758,7 +777,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
 #pragma unroll
             for (int sl = 0; sl < kSlots; sl++) {
                 e[sl] = 0;
-                if (st[sl] == 1 && lane == 0)
+                if (st[sl] == 1 && lane_id<RM>() == 0)
                     e[sl] = __hip_atomic_load(&w.entry[(long long)tt[sl] * nsg + tq[sl]], __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -782,7 +801,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
 #pragma unroll
                 for (int sl = 0; sl < kSlots; sl++)
                     if (st[sl] == 1) {
-                        if (lane == 0) atomicAdd(w.err, 1);
+                        if (lane_id<RM>() == 0) atomicAdd(w.err, 1);
                         start(sl, j0[sl]);
                     }
                 idle = 0;
@@ -796,14 +815,14 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
 #pragma unroll
         for (int i = 0; i < SC_ABL_EXTRA_RT; i++) {
             int v = 0;  // (word 1 of this XCD's queue line: unused, stays 0)
-            if (lane == 0) v = atomicAdd(&a.queues[(q * kSubQ + u) * kQueueStride + 1], 0);
+            if (lane_id<RM>() == 0) v = atomicAdd(&a.queues[(q * kSubQ + u) * kQueueStride + 1], 0);
             v = __builtin_amdgcn_readfirstlane(v);
             if (v == 0x7fffffff) drained = true;
         }
 #endif
 #pragma unroll
         for (int sl = 0; sl < kSlots; sl++) {
-            if (lane == 0) {
+            if (lane_id<RM>() == 0) {
                 SlotDesc dd{};
                 if (st[sl] == 2) {
                     const LevelInfo &L = Lv[level[sl]];
@@ -835,12 +854,12 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
         for (int sl = 0; sl < kSlots; sl++)
 #pragma unroll
             for (int c = 0; c < kBatchChunks; c++) {
-                const int u = c * 64 + lane;
+                const int u = c * 64 + lane_id<RM>();
                 mine[sl][c] = __ballot(st[sl] == 2 && u < desc[sl].nw && need(sl * kBatch + u));
             }
         // park the slot state in LDS across the evaluation: it would otherwise
         // stay live in SGPRs / VGPR lanes through the register-heavy item loop
-        if (lane == 0) {
+        if (lane_id<RM>() == 0) {
 #pragma unroll
             for (int sl = 0; sl < kSlots; sl++) {
                 int *pk = park + sl * 10;
@@ -852,11 +871,11 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
         wave_sync();
         SC_PROF(c_setup);
 #if SC_PROF_CHAIN
-        eval_windows<LW>(a, B, reinterpret_cast<const char *>(a.table), Wl, Bl, Ol, P, st_s, surv,
-                         st_p, lane, need, istats);
+        eval_windows<LW, RM>(a, B, reinterpret_cast<const char *>(a.table), Wl, Bl, Ol, P, st_s, surv,
+                         st_p, 0, need, istats);
 #else
-        eval_windows<LW>(a, B, reinterpret_cast<const char *>(a.table), Wl, Bl, Ol, P, st_s, surv,
-                         st_p, lane, need);
+        eval_windows<LW, RM>(a, B, reinterpret_cast<const char *>(a.table), Wl, Bl, Ol, P, st_s, surv,
+                         st_p, 0, need);
 #endif
         wave_sync();
         SC_PROF(c_eval);
@@ -891,8 +910,8 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
             float *sg = s_seg(sl);
 #pragma unroll
             for (int c = 0; c < kBatchChunks; c++) {
-                if (!((mine[sl][c] >> lane) & 1ull)) continue;
-                const int u = c * 64 + lane;
+                if (!((mine[sl][c] >> lane_id<RM>()) & 1ull)) continue;
+                const int u = c * 64 + lane_id<RM>();
                 const int k = r[sl] + 2 * u, p = st_p[sl * kBatch + u];
                 const float sc = st_s[sl * kBatch + u];
                 bool good = false;
@@ -938,7 +957,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
                 } else if (qg < 64) {  // lands on good window qg, continues at qg + 1
                     vis = path & (qg == 63 ? ~0ull : ((2ull << qg) - 1ull));
                     const int k = (c << 6) + qg;
-                    if (lane == 0 && ((dtw >> qg) & 1ull)) {  // detection (:203)
+                    if (lane_id<RM>() == 0 && ((dtw >> qg) & 1ull)) {  // detection (:203)
                         const int slot = atomicAdd(&w.counters[0], 1);
                         atomicAdd(&w.counters[1 + w.frame0 + fr], 1);
                         if (slot < w.capacity) {
@@ -962,7 +981,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
                     else rr = ((c + 1) << 6) + (b & 1);
                 }
                 nvis[sl] += __popcll(vis);
-                if (w.dbg_v && ((vis >> lane) & 1ull)) w.dbg_v[gi0 + (c << 6) + lane] = 1;
+                if (w.dbg_v && ((vis >> lane_id<RM>()) & 1ull)) w.dbg_v[gi0 + (c << 6) + lane_id<RM>()] = 1;
                 if (f < qg || rr >= ns) break;
             }
             r[sl] = rr;
@@ -972,7 +991,7 @@ __global__ __launch_bounds__(kChainThreads, SC_CHAIN_MIN_WGS) void chain_kernel(
         SC_PROF(c_merge);
     }
 #if SC_PROF_CHAIN
-    if (w.prof && lane == 0) {
+    if (w.prof && lane_id<RM>() == 0) {
         atomicAdd(&w.prof[0], c_idle);
         atomicAdd(&w.prof[1], c_setup);
         atomicAdd(&w.prof[2], c_eval);
@@ -1023,28 +1042,49 @@ void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s) {
 }
 
 int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hipStream_t s) {
-    const size_t scratch = kChainWaves * chain_wave_bytes(w.row_max) + w.n_levels * sizeof(LevelInfo);
-    bool lw = model_lds_bytes(a.K, true) + scratch <= 160 * 1024;
+    auto scratch = [&](int nw) { return nw * chain_wave_bytes(w.row_max) + w.n_levels * sizeof(LevelInfo); };
+    const size_t kLds = 160 * 1024;
+    // 16 waves with the weights in LDS when they fit and a frame's table sits
+    // comfortably in the 256 MiB Infinity Cache; else 12 (weights in LDS when
+    // they fit: measured faster even where it costs occupancy).  More waves
+    // help the latency-bound narrow levels (C2 levels 0-12: -3 %) and hurt the
+    // wide ones, whose gathers already saturate the Infinity-Cache fabric
+    // (levels 13-23 alone: 106 % of the measured gather ceiling, +12 % at 16
+    // waves); a 4K frame's 265 MB table leaves the Infinity Cache (C4: +8 %
+    // at 16 waves).  C2 as a whole: -2.7 % (profiles/r3/g3).
+    const bool fabric_bound = a.g.frame4 * 16 > (128ll << 20);
+    int nw = !fabric_bound && model_lds_bytes(a.K, true) + scratch(16) <= kLds ? 16 : 12;
+    if (c.chain_waves == 12 || (c.chain_waves == 16 && model_lds_bytes(a.K, false) + scratch(16) <= kLds))
+        nw = c.chain_waves;  // SC_OPT_CHAIN_WAVES
+    bool lw = model_lds_bytes(a.K, true) + scratch(nw) <= kLds;
     if (c.lds_weights >= 0) lw = lw && c.lds_weights != 0;  // SC_OPT_LDS_WEIGHTS
-    const size_t lds = model_lds_bytes(a.K, lw) + scratch;
+    const size_t lds = model_lds_bytes(a.K, lw) + scratch(nw);
+    const int nt = 64 * nw;
     int per_cu = 0;
-    if (lw)
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<true>, kChainThreads, lds);
+    if (nw == 16 && lw)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<true, 16>, nt, lds);
+    else if (nw == 16)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<false, 16>, nt, lds);
+    else if (lw)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<true, 12>, nt, lds);
     else
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<false>, kChainThreads, lds);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<false, 12>, nt, lds);
     per_cu = std::max(1, std::min(per_cu, 4));
     if (c.wgs_per_cu > 0) per_cu = std::min(per_cu, c.wgs_per_cu);  // SC_OPT_WGS_PER_CU
     const int grid = std::max(1, c.cus) * per_cu;
-    if (lw)
-        hipLaunchKernelGGL(chain_kernel<true>, dim3(grid), dim3(kChainThreads), lds, s, a, w);
+    if (nw == 16 && lw)
+        hipLaunchKernelGGL((chain_kernel<true, 16>), dim3(grid), dim3(nt), lds, s, a, w);
+    else if (nw == 16)
+        hipLaunchKernelGGL((chain_kernel<false, 16>), dim3(grid), dim3(nt), lds, s, a, w);
+    else if (lw)
+        hipLaunchKernelGGL((chain_kernel<true, 12>), dim3(grid), dim3(nt), lds, s, a, w);
     else
-        hipLaunchKernelGGL(chain_kernel<false>, dim3(grid), dim3(kChainThreads), lds, s, a, w);
+        hipLaunchKernelGGL((chain_kernel<false, 12>), dim3(grid), dim3(nt), lds, s, a, w);
     return grid;
 }
 
-size_t chain_lds_bytes(int K, int row_max, int n_levels) {  // smallest variant
-    return model_lds_bytes(K, false) + kChainWaves * chain_wave_bytes(row_max) +
-           n_levels * sizeof(LevelInfo);
+size_t chain_lds_bytes(int K, int row_max, int n_levels) {  // smallest variant (12 waves, weights via caches)
+    return model_lds_bytes(K, false) + 12 * chain_wave_bytes(row_max) + n_levels * sizeof(LevelInfo);
 }
 
 size_t cascade_lds_bytes(int K, int strip_max, int band_rows) {  // smallest variant

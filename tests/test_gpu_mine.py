@@ -161,3 +161,25 @@ def test_first_round_small_images(sc, oracle, W, H):
     ref = oracle.mine(oracle.integral(img), oracle.empty_cascade(), 64)
     _check(got, ref)
     assert (got[2] == 0) == (min(W, H) < 40)
+
+
+def test_capacity_far_above_candidates(sc, oracle, face_cascade):
+    """A trainer-style capacity (FillNegSamples' n_total) far above the
+    candidates found: the descriptors are the oracle's, and the host-output
+    path sizes its device descriptor buffer to the kept windows, not to the
+    capacity (100 000 x 608 x 32 floats would be 7.8 GB)."""
+    import torch
+    from surfcascade_amd import synth
+    c = face_cascade
+    theta = np.full(c.n_stages, 0.42, np.float32)
+    text = synth.write_cfg(synth.cascade_tree(c.n_weak, theta, c.patch_index, c.w, c.bias))
+    img = _frame(480, 360, 17)
+    m = sc.Miner(sc.Model.parse(text))
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info(0)[0]
+    got = m.mine(img, 100000)
+    free1 = torch.cuda.mem_get_info(0)[0]
+    ref = oracle.mine(oracle.integral(img), oracle.cascade_from_cfg(text), 100000)
+    _check(got, ref)
+    assert 0 < got[2] < 100000
+    assert free0 - free1 < (1 << 30), "descriptor buffer sized to the capacity"

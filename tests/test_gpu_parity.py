@@ -120,6 +120,62 @@ def test_chain_row_orders(sc, oracle, face_cascade, order, block):
                  oracle.Params(n_levels=8), **opts)
 
 
+@pytest.mark.parametrize("phases,wgs,full", [("1", None, None), ("1", None, "1"), ("2", None, "1"),
+                                              (None, "1", None), (None, "1", "1"), (None, "2", "1")])
+def test_phase_planes_and_workgroups(sc, oracle, face_cascade, phases, wgs, full):
+    """SC_OPT_PHASES (one or two phase planes per step: the chain kernel's
+    per-item column mapping takes the ph == step branch with 1) and
+    SC_OPT_WGS_PER_CU, on both window kernels: the schedule and layout
+    change, the bits do not."""
+    opts = {k: int(v) for k, v in (("phases", phases), ("wgs_per_cu", wgs), ("full_grid", full)) if v}
+    img = _frame(1280, 720, 80)
+    _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=8),
+                 oracle.Params(n_levels=8), **opts)
+
+
+@pytest.mark.parametrize("waves,lw", [("12", None), ("16", None), ("16", "0"), ("12", "0")])
+def test_chain_waves(sc, oracle, face_cascade, waves, lw):
+    """SC_OPT_CHAIN_WAVES: the 12-wave (3 per SIMD) and 16-wave (4 per SIMD,
+    rematerialised lane values, 128 VGPRs) chain kernels, with the weights in
+    LDS or read through the caches, give the oracle's bits."""
+    opts = {"chain_waves": int(waves)}
+    if lw:
+        opts["lds_weights"] = int(lw)
+    img = _frame(1280, 720, 82)
+    _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=8),
+                 oracle.Params(n_levels=8), **opts)
+
+
+@pytest.mark.parametrize("lo,hi", [(2, 5), (6, 0)])
+def test_level_range_scan(sc, oracle, face_cascade, lo, hi):
+    """SC_OPT_LEVEL_LO / _HI (level-group profiling) scan exactly the levels
+    [lo, hi): their windows, visited set and detections are the oracle's, the
+    other levels are neither evaluated nor visited."""
+    img = _frame(1280, 720, 81)
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=8)).set_options(level_lo=lo, level_hi=hi)
+    det.set_debug(True)
+    wins = det.detect(img)
+    p, s, v = det.dump_grid()
+    params = oracle.Params(n_levels=8)
+    T = oracle.integral(img)
+    rp, rs = oracle.eval_grid(T, face_cascade, params)
+    layout, _ = oracle.grid_layout(1280, 720, params)
+    rv, _ = oracle.walk_grid(rp, rs, layout, face_cascade.n_stages, params.stride_score)
+    inr = np.zeros(len(p), bool)
+    for (lv, _l, _lh, nx, ny, base) in layout:
+        if lv >= lo and (hi == 0 or lv < hi):
+            inr[base:base + nx * ny] = True
+    assert (p[~inr] == -2).all() and (v[~inr] == 0).all()
+    ev = (p != -2) & inr
+    np.testing.assert_array_equal(p[ev], rp[ev])
+    np.testing.assert_array_equal(v[inr], rv[inr])
+    assert det.info("visited") == int(rv[inr].sum())
+    ref, _ = oracle.detect(T, face_cascade, params)
+    ref = [r for r in ref if r["level"] >= lo and (hi == 0 or r["level"] < hi)]
+    assert len(ref) > 0 or hi != 0
+    assert _det_set(wins) == _det_set(ref)
+
+
 @pytest.mark.parametrize("n", [2, 3, 4])
 def test_integral_batch_frames(sc, oracle, n):
     """Every frame of a batch: 2 and 3 frames take the two-pass integral
