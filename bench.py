@@ -47,6 +47,13 @@ MODELS = os.path.join(ROOT, "surfcascade_amd", "models")
 # 8 4K frames per step for the same reason (6.49 vs 6.18 G windows/s at 4),
 # C5 32 like C2 (3.81 vs 3.58 at 16).
 CONFIGS = {
+    # C1: the reference's CPU plumbing case -- no GPU; bench.py --config C1
+    # prints the CPU restatement's line alone (the cpu_baseline legs)
+    "C1": dict(width=640, height=480, levels=1, batch=8, model="face40_synth.cfg",
+               pedestrian=False,
+               metric="detection windows/sec, 640x480 single scale, CPU reference path",
+               desc="C1: %dx%d frames, %d level (l=70..%d), 40x40 face cascade 10 stages / 190 weak LR; "
+                    "%d seeded frames, CPU only"),
     "C2": dict(width=1920, height=1080, levels=24, batch=32, model="face40_synth.cfg",
                pedestrian=False,
                metric="detection windows/sec on 1080p 24-scale pyramid",
@@ -162,7 +169,9 @@ def cpu_baseline(frames, model_path, levels, seconds, pedestrian=False):
                 break
         dt = time.perf_counter() - t0
         res[nt] = (done * grid / dt, done, dt)
-    threads = max(legs, key=lambda nt: res[nt][0])
+    # the fastest leg is the baseline (C1's single level gives OpenMP over
+    # levels one level to share: one thread wins there)
+    threads = max(res, key=lambda nt: res[nt][0])
     v, done, dt = res[threads]
     v1, done1, dt1 = res[1]
     return {"value": v, "unit": "windows/s", "cores": threads, "kind": "port",
@@ -251,8 +260,31 @@ class StubDetector:
         return []
 
 
+def cpu_only_line(args):
+    """--config C1: the CPU plumbing case (BASELINE.json configs[0]) -- the
+    oracle's reference loop on in-memory frames (ObjDetector.cpp:157-158,
+    246-250 bracket, decode and I/O excluded), all host cores, the cgroup
+    quota and 1 thread; no GPU is touched."""
+    import surfcascade_amd as sc
+    from surfcascade_amd import synth
+    W, H, B = args.width, args.height, args.batch
+    frames = synth.make_frames(W, H, B, seed0=1000)
+    params = sc.ScanParams(n_levels=args.levels)
+    cb = cpu_baseline(frames, args.model, args.levels, args.cpu_seconds)
+    line = {"metric": CONFIGS[args.config]["metric"], "value": cb["value"], "unit": "windows/s",
+            "n_gpus": 0, "higher_is_better": True, "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded %dx%d frames, seeded 10-stage 40x40 cascade)" % (W, H),
+            "config": {"workload": CONFIGS[args.config]["desc"] % (W, H, args.levels,
+                                                                   params.level_len(args.levels - 1), B),
+                       "name": args.config, "levels": args.levels},
+            "cpu_baseline": cb}
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
+    if args.config == "C1":
+        return cpu_only_line(args)
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
         sys.exit(launch_ranks(args))

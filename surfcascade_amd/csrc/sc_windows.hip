@@ -81,6 +81,17 @@ __device__ __forceinline__ int lane_id() {
     }
 }
 
+// A row descriptor read through the scalar cache: the row list is written by
+// the host before the launch and only read here, and the scalar path keeps
+// this dependent round trip out of the vector-memory pipe, which the item
+// gathers keep busy (TD ~96 %): a vector load queues behind them.
+__device__ __forceinline__ int2 row_desc(const int2 *rows, int i) {
+    // the constant address space: a wave-uniform address becomes an s_load
+    typedef __attribute__((address_space(4))) const unsigned long long cu64;
+    const unsigned long long v = ((cu64 *)(unsigned long long)rows)[i];
+    return make_int2((int)(unsigned)v, (int)(unsigned)(v >> 32));
+}
+
 // popcount of the bits of m below this lane (v_mbcnt: no 64-bit lane mask held)
 __device__ __forceinline__ int popc_below(unsigned long long m) {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
@@ -249,28 +260,32 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
     // 1) prefilter; survivors in (row, x) order
     [[maybe_unused]] unsigned long long t_pre0 = 0;
     if constexpr (std::remove_reference_t<Stats>::on) t_pre0 = __builtin_amdgcn_s_memtime();
-    int nsurv = 0;
-    for (int r = 0; r < B.rows(); r++) {
-        const int nw = B.width(r), pre_row = B.pre_row_of(r);
-        const float thr = B.thr_of(r);
-        for (int b = 0; b < nw; b += 64) {
-            const int u = b + lane_id<RM>();
-            bool pass = false;
-            if (u < nw && need(r * stride + u)) {
-                const int pre_col = B.pre_col_of(r, u);
-                const float4 *t0 = T + B.origin(r, u);
-                const float4 v = box4(t0[0], t0[pre_row + pre_col], t0[pre_col], t0[pre_row]);
-                const float m = (((v.x + v.y) + v.z) + v.w) / 2.0f;  // sum(), :351-358
-                pass = m > thr;                                      // ObjDetector.cpp:188
-                st_p[r * stride + u] = pass ? 0 : -1;
-                st_s[r * stride + u] = 0.0f;
-            }
-            const unsigned long long mk = __ballot(pass);
-            if (pass) surv[nsurv + popc_below(mk)] = ((unsigned)r << 16) | (unsigned)u;
-            nsurv += __popcll(mk);
-            if constexpr (std::remove_reference_t<Stats>::on)
-                stats.pre(__popcll(__ballot(u < nw && need(r * stride + u))), __popcll(mk));
+    // The rows' windows flattened into one list of 64-lane chunks (the chain
+    // kernel's two slots hold ~35 windows each: one set of 4 corner loads
+    // instead of one per slot)
+    int nsurv = 0, tot = 0;
+    for (int r = 0; r < B.rows(); r++) tot += B.width(r);
+    for (int b = 0; b < tot; b += 64) {
+        int u = b + lane_id<RM>(), r = 0;
+        while (r + 1 < B.rows() && u >= B.width(r)) {
+            u -= B.width(r);
+            r++;
         }
+        const bool act = b + lane_id<RM>() < tot && need(r * stride + u);
+        bool pass = false;
+        if (act) {
+            const int pre_row = B.pre_row_of(r), pre_col = B.pre_col_of(r, u);
+            const float4 *t0 = T + B.origin(r, u);
+            const float4 v = box4(t0[0], t0[pre_row + pre_col], t0[pre_col], t0[pre_row]);
+            const float m = (((v.x + v.y) + v.z) + v.w) / 2.0f;  // sum(), :351-358
+            pass = m > B.thr_of(r);                              // ObjDetector.cpp:188
+            st_p[r * stride + u] = pass ? 0 : -1;
+            st_s[r * stride + u] = 0.0f;
+        }
+        const unsigned long long mk = __ballot(pass);
+        if (pass) surv[nsurv + popc_below(mk)] = ((unsigned)r << 16) | (unsigned)u;
+        nsurv += __popcll(mk);
+        if constexpr (std::remove_reference_t<Stats>::on) stats.pre(__popcll(__ballot(act)), __popcll(mk));
     }
     wave_sync();
     if constexpr (std::remove_reference_t<Stats>::on) stats.pre_cyc += __builtin_amdgcn_s_memtime() - t_pre0;
@@ -702,7 +717,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             if (v < n_tasks) {
                 t = v;
                 qq = 0;
-                rd = w.rows[v % w.n_rows];
+                rd = row_desc(w.rows, v % w.n_rows);
                 return true;
             }
             pre = 0;
@@ -714,7 +729,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             if (v < n_tasks) {
                 t = v;
                 qq = q >> sh;  // the segment
-                rd = w.rows[v % w.n_rows];
+                rd = row_desc(w.rows, v % w.n_rows);
                 return true;
             }
             if (++empty == kXcds * kSubQ) {  // every sub-queue drained
