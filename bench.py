@@ -537,6 +537,11 @@ def roofline(achieved, traffic, valu_insts, avg_win_s, bytes_launch, pipe_bytes,
         r["fabric_frac"] = miss / avg_win_s / ceil
         hit = pmc["counters_per_launch"].get("TCC_HIT_sum")
         r["l2_hit"] = hit / (hit + miss) if hit else None
+        # a table beyond the Infinity Cache (C4) gathers from HBM: the same
+        # shape's cold-HBM ceiling (profiles/calib k_sparse)
+        hceil = pmc.get("hbm_gather_ceiling_lines_per_s")
+        if hceil:
+            r["hbm_gather_frac"] = miss / avg_win_s / hceil
     return r
 
 

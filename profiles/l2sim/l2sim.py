@@ -46,7 +46,8 @@ def geometry(W, H, step=3, layout="split"):
     return Geom(W, H, step, ph, Qp, rowp, 1, 2)
 
 
-def build_tasks(O, casc, img, n_levels, lo, hi, row_block, nseg, order, big_split=None, big_from=13):
+def build_tasks(O, casc, img, n_levels, lo, hi, row_block, nseg, order, big_split=None, big_from=13,
+                xcd_split=None):
     H, W = img.shape
     P = O.Params(n_levels=n_levels)
     T = O.integral(img)
@@ -73,6 +74,8 @@ def build_tasks(O, casc, img, n_levels, lo, hi, row_block, nseg, order, big_spli
         ns, rc = nseg, 1
         if big_split and lv >= big_from:  # big levels: ns column segments x rc row classes
             ns, rc = big_split
+        if xcd_split:  # small levels on XCDs [0, n_small), big ones on [n_small, 8)
+            ns = xcd_split if lv < big_from else 8 - xcd_split
         nxs = (nx + ns - 1) // ns
         for sg in range(ns):
             j0, j1 = min(nx, sg * nxs), min(nx, (sg + 1) * nxs)
@@ -93,7 +96,10 @@ def build_tasks(O, casc, img, n_levels, lo, hi, row_block, nseg, order, big_spli
                 parts.append(it)
             if parts:
                 chunks.append(np.concatenate(parts))
-                xcd.append(sg * 8 // ns + ((y // step) % rc) * (8 // ns // rc) if rc > 1 else sg * 8 // ns)
+                if xcd_split:
+                    xcd.append(sg if lv < big_from else xcd_split + sg)
+                else:
+                    xcd.append(sg * 8 // ns + ((y // step) % rc) * (8 // ns // rc) if rc > 1 else sg * 8 // ns)
     lens = np.array([len(c) for c in chunks], np.int64)
     it_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     items = np.ascontiguousarray(np.concatenate(chunks))
@@ -112,6 +118,7 @@ def main():
     ap.add_argument("--seed", type=int, default=1000)
     ap.add_argument("--big-split", help="big levels: SEGS:ROWCLASSES (e.g. 4:2)")
     ap.add_argument("--big-from", type=int, default=13)
+    ap.add_argument("--xcd-split", type=int, help="small levels on this many XCDs, big on the rest")
     ap.add_argument("--big-slots", type=int, default=-1,
                     help="two queues: only this many of the conc slots take big-level tasks")
     a = ap.parse_args()
@@ -123,7 +130,7 @@ def main():
     t0 = time.time()
     bs = tuple(int(v) for v in a.big_split.split(":")) if a.big_split else None
     items, it_off, xcd, layout = build_tasks(O, casc, img, 24, lo, hi, a.row_block, a.nseg, a.order, bs,
-                                             a.big_from)
+                                             a.big_from, a.xcd_split)
     t1 = time.time()
     patches = O.extract_patches(casc.tmpl_w, casc.tmpl_h)
     rects = patches[casc.patch_index]

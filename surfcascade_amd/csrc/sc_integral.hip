@@ -33,6 +33,9 @@ namespace {
 #define SC_COL_UNROLL 16
 #endif
 constexpr int kColUnroll = SC_COL_UNROLL;  // rows per colstrip block (two blocks of loads in flight)
+#ifndef SC_COL_WAVES  // colstrip: waves per SIMD the register budget must allow
+#define SC_COL_WAVES 1
+#endif
 
 __device__ __forceinline__ uint32_t sat_sub(uint32_t a, uint32_t b) { return a > b ? a - b : 0u; }
 
@@ -163,7 +166,7 @@ __device__ __forceinline__ ColBlock col_block() {
 
 // One wave per (frame, 64-column strip, channel half): lane = column, so a
 // row's stores are long runs within each phase plane of the half.
-__global__ __launch_bounds__(64) void colstrip_kernel(RowScanArgs a) {
+__global__ __launch_bounds__(64, SC_COL_WAVES) void colstrip_kernel(RowScanArgs a) {
     const ColBlock cb_ = col_block();
     const int s = cb_.s, h = cb_.h, frame = cb_.frame, lane = threadIdx.x;
     const TableGeom g = a.g;
