@@ -92,6 +92,29 @@ __device__ __forceinline__ int2 row_desc(const int2 *rows, int i) {
     return make_int2((int)(unsigned)v, (int)(unsigned)(v >> 32));
 }
 
+// Bit i of m -> bit base + 2i of the bit array w (i < 64: the positions
+// k = r + 2u of a batch chunk's windows): the 32-bit halves of m spread to
+// every second bit of a 64-bit word, each ORed in at its offset.
+__device__ __forceinline__ unsigned long long spread32(unsigned long long x) {
+    x &= 0xffffffffull;
+    x = (x | (x << 16)) & 0x0000ffff0000ffffull;
+    x = (x | (x << 8)) & 0x00ff00ff00ff00ffull;
+    x = (x | (x << 4)) & 0x0f0f0f0f0f0f0f0full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+__device__ __forceinline__ void or_word(unsigned long long *w, int bit, unsigned long long e) {
+    if (!e) return;
+    const int wd = bit >> 6, sh = bit & 63;
+    atomicOr(&w[wd], e << sh);
+    if (sh && (e >> (64 - sh))) atomicOr(&w[wd + 1], e >> (64 - sh));
+}
+__device__ __forceinline__ void or_spread(unsigned long long *w, int base, unsigned long long m) {
+    or_word(w, base, spread32(m));
+    or_word(w, base + 64, spread32(m >> 32));
+}
+
 // popcount of the bits of m below this lane (v_mbcnt: no 64-bit lane mask held)
 __device__ __forceinline__ int popc_below(unsigned long long m) {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
@@ -925,22 +948,36 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             float *sg = s_seg(sl);
 #pragma unroll
             for (int c = 0; c < kBatchChunks; c++) {
-                if (!((mine[sl][c] >> lane_id<RM>()) & 1ull)) continue;
+                const unsigned long long mk = mine[sl][c];
+                if (!mk) continue;
+                const bool in = (mk >> lane_id<RM>()) & 1ull;
                 const int u = c * 64 + lane_id<RM>();
-                const int k = r[sl] + 2 * u, p = st_p[sl * kBatch + u];
-                const float sc = st_s[sl * kBatch + u];
-                bool good = false;
-                if (p >= 0) {
-                    const double fin = ((double)sc + p + 1) / S;  // ObjDetector.cpp:201
-                    good = !(fin < w.stride_score);               // :214
+                const int k = r[sl] + 2 * u;
+                bool good = false, det = false;
+                if (in) {
+                    const int p = st_p[sl * kBatch + u];
+                    const float sc = st_s[sl * kBatch + u];
+                    if (p >= 0) {
+                        const double fin = ((double)sc + p + 1) / S;  // ObjDetector.cpp:201
+                        good = !(fin < w.stride_score);               // :214
+                    }
+                    det = p == S;  // passed every stage
+                    sg[k] = sc;
+                    if (a.st_p) {  // debug: per-window results for the parity dumps
+                        a.st_p[gi0 + k] = (int8_t)p;
+                        a.st_s[gi0 + k] = sc;
+                    }
                 }
-                sg[k] = sc;
-                atomicOr(&ev_[k >> 6], 1ull << (k & 63));
-                if (good) atomicOr(&gd_[k >> 6], 1ull << (k & 63));
-                if (p == S) atomicOr(&dt_[k >> 6], 1ull << (k & 63));  // passed every stage
-                if (a.st_p) {  // debug: per-window results for the parity dumps
-                    a.st_p[gi0 + k] = (int8_t)p;
-                    a.st_s[gi0 + k] = sc;
+                // the chunk's windows sit at k = r + 2u: their evaluated / good /
+                // detection bits, spread to every second bit, written by one
+                // lane (per-lane 64-bit LDS atomics on one or two words were
+                // the kernel's LDS bank conflicts)
+                const unsigned long long gm = __ballot(good), dm = __ballot(det);
+                if (lane_id<RM>() == 0) {
+                    const int base = r[sl] + 128 * c;
+                    or_spread(ev_, base, mk);
+                    if (gm) or_spread(gd_, base, gm);
+                    if (dm) or_spread(dt_, base, dm);
                 }
             }
             wave_sync();
