@@ -192,7 +192,7 @@ int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, 
 int sc_detector_info(sc_detector *d, int what, int64_t *value);
 
 /* ---- tuning and test options ---------------------------------------------
- * Options 1-14 and 17 are schedule / layout choices that never change a result bit
+ * Options 1-14 and 17-19 are schedule / layout choices that never change a result bit
  * (tests/test_gpu_parity.py runs each against the oracle); the defaults are
  * the measured-fastest.  Options 15-16 restrict the scan to a range of levels
  * (profiling of level groups): they DO change the result, to the windows of
@@ -223,8 +223,14 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
 #define SC_OPT_LEVEL_LO 15    /* scan only levels >= LEVEL_LO (default 0)      */
 #define SC_OPT_LEVEL_HI 16    /* ... and < LEVEL_HI (0: every level)           */
 #define SC_OPT_CHAIN_WAVES 17 /* chain kernel waves per CU: 0 auto (16 when the  */
-                              /* model and their scratch fit the LDS and a     */
-                              /* frame's table is <= 128 MiB), 12, 16          */
+                              /* model and their scratch fit the LDS, a        */
+                              /* frame's table is <= 128 MiB and the launch    */
+                              /* has 2+ frames), 12, 16                        */
+#define SC_OPT_INTEGRAL_FUSE 18 /* integral column walks inside the chain      */
+                              /* kernel: 0 auto (from 4 frames per launch),    */
+                              /* 1 never, 2 whenever a launch has 2+ frames    */
+#define SC_OPT_INTEGRAL_PRE 19 /* fused: frames per launch integrated before   */
+                              /* the chain kernel (0: default 2)               */
 int sc_detector_set_option(sc_detector *d, int option, int64_t value);
 
 /* Enable per-window debug records (grid order) for the next detect calls. */

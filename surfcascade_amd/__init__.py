@@ -41,13 +41,14 @@ RECT_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("width", "<i4"), ("height", 
 
 KERNELS = ("rowscan", "colscan", "windows", "walk")
 
-# sc_detector_set_option keys (include/surfcascade.h SC_OPT_*): 1-14 and 17
+# sc_detector_set_option keys (include/surfcascade.h SC_OPT_*): 1-14 and 17-19
 # are schedule and layout choices that never change a result bit; level_lo /
 # level_hi restrict the scan to the levels [lo, hi) (level-group profiling)
 OPTIONS = {"full_grid": 1, "chunk_min": 2, "table_layout": 3, "phases": 4, "substrips": 5,
            "band_rows": 6, "row_order": 7, "row_block": 8, "chain_chunk": 9, "lds_weights": 10,
            "wgs_per_cu": 11, "profile": 12, "chain_segs": 13, "integral_passes": 14,
-           "level_lo": 15, "level_hi": 16, "chain_waves": 17}
+           "level_lo": 15, "level_hi": 16, "chain_waves": 17,
+           "integral_fuse": 18, "integral_pre": 19}
 
 # every symbol include/surfcascade.h declares
 EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_model_save",

@@ -128,6 +128,8 @@ struct sc_detector {
         int lds_weights = -1, wgs_per_cu = 0, profile = 0, chain_segs = 0, integral_passes = 0;
         int level_lo = 0, level_hi = 0;  // scan only levels [lo, hi) (hi 0: all)
         int chain_waves = 0;             // chain kernel waves per workgroup (0 auto)
+        int integral_fuse = 0;           // column walks inside the chain kernel: 0 auto, 1 never, 2 from 2 frames
+        int integral_pre = 0;            // fused: frames integrated before the chain kernel (0: 2)
     } opt;
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
@@ -603,7 +605,22 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     const bool lazy = d->lazy && sc::chain_lds_bytes(d->K, seg_max, g.n_levels) <= 160 * 1024;
     const size_t n_rows = g.rows.size();
     const bool chain = n_rows > 0 && lazy && !d->miner;
-    if (chain) d->d_entry.ensure(n_rows * std::min(chunk, n) * sc::kXcds + 1);
+    // hand-off words of a chain launch: [rows x frames x kXcds] entries, the
+    // watchdog word, then the fused integral's walk counter and per-frame
+    // walk counts (WalkArgs::int_ctl); sized for the largest launch
+    auto entry_words = [&](int frames) { return (long long)n_rows * frames * sc::kXcds + 2 + frames; };
+    if (chain) d->d_entry.ensure((size_t)entry_words(std::min(chunk, n)));
+    // Fused integral (SC_OPT_INTEGRAL_FUSE): the first `pre` frames of every
+    // launch are integrated by their own kernels (2 by default: a frame's 60
+    // walks inside the chain kernel take longer than the chain takes over
+    // frame 0, 13.63 vs 13.74 ms chain kernel at C2, profiles/r3/g10), the
+    // column walks of the others run inside the chain kernel as a second
+    // task type, overlapping the gathers.  Auto: from
+    // 4 frames per launch, where colstrip would be the integral's column pass.
+    const int pre = d->opt.integral_pre > 0 ? d->opt.integral_pre : 2;
+    const int fuse_from = d->opt.integral_fuse == 2 ? 2 : 4;
+    const bool fuse = chain && d->opt.integral_fuse != 1 && std::min(chunk, n) >= fuse_from &&
+                      std::min(chunk, n) > pre;
 
     sc::RowScanArgs ra{d_frames, (long long)H * stride, stride, d->d_table.p, g.tg, d->d_carry.p, {}, {}};
     // zeroed by rowcarry (stream order: before every kernel that uses them):
@@ -619,7 +636,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
         ra.zero[2] = reinterpret_cast<int *>(d->d_visited.p);
         ra.zero_n[2] = (long long)n_rows * n;
         ra.zero[3] = d->d_entry.p;
-        ra.zero_n[3] = (long long)n_rows * std::min(chunk, n) * sc::kXcds + 1;
+        ra.zero_n[3] = entry_words(std::min(chunk, n));
     }
     hipEvent_t e0 = nullptr;
     timed_begin(d, &e0);
@@ -630,8 +647,24 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     timed_begin(d, &e0);
     // colstrip's 60 waves per frame walk every row: for up to three frames the
     // row-parallel two-pass form is shorter (SC_OPT_INTEGRAL_PASSES overrides)
-    const bool two_pass = d->opt.integral_passes ? d->opt.integral_passes == 2 : n <= 3;
-    sc::launch_colscan(ra, n, two_pass, d->stream);
+    const long long carry_frame = (long long)H * ((W + sc::kStrip - 1) / sc::kStrip) * 8;  // u32 per frame
+#if defined(SC_WALK_STORE) && SC_WALK_STORE == 0  // timing ablation: walks store nothing, tables built here
+    if (false) {
+#else
+    if (fuse) {  // only the first `pre` frames of each launch here
+#endif
+        const bool two_pass = d->opt.integral_passes ? d->opt.integral_passes == 2 : pre <= 3;
+        for (int f0 = 0; f0 < n; f0 += chunk) {
+            sc::RowScanArgs rc = ra;
+            rc.frames = d_frames + (long long)f0 * H * stride;
+            rc.table = d->d_table.p + (size_t)f0 * g.tg.frame4;
+            rc.carry = d->d_carry.p + f0 * carry_frame;
+            sc::launch_colscan(rc, std::min(pre, n - f0), two_pass, d->stream);
+        }
+    } else {
+        const bool two_pass = d->opt.integral_passes ? d->opt.integral_passes == 2 : n <= 3;
+        sc::launch_colscan(ra, n, two_pass, d->stream);
+    }
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_COLSCAN, e0);
 
@@ -706,6 +739,16 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             wc.entry = d->d_entry.p;
             d->err_word = (long long)(n_rows * std::min(chunk, n) * sc::kXcds);
             wc.err = d->d_entry.p + d->err_word;
+            wc.int_ctl = wc.err + 1;
+            if (fuse && nc > pre) {
+                wc.frames = d_frames + (long long)f0 * H * stride;
+                wc.frame_bytes = (long long)H * stride;
+                wc.stride = stride;
+                wc.carry = d->d_carry.p + f0 * carry_frame;
+                wc.int_f0 = pre;
+                wc.walks_per_frame = 2 * ((W + 2 * sc::kStrip - 1) / (2 * sc::kStrip));
+                wc.int_walks = (nc - pre) * wc.walks_per_frame;
+            }
             wc.frame0 = f0;
             wc.nseg = segs_for(nc);
             wc.seg_shift = wc.nseg == 8 ? 0 : wc.nseg == 4 ? 1 : wc.nseg == 2 ? 2 : 3;
@@ -718,7 +761,9 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
                 wc.prof = d->d_prof.p;
             }
             if (f0 > 0) {  // (the first chunk's were cleared by rowcarry)
-                HIPCHK(hipMemsetAsync(d->d_entry.p, 0, sizeof(int) * (n_rows * nc * sc::kXcds + 1), d->stream));
+                // (the watchdog word between them keeps counting over the launches)
+                HIPCHK(hipMemsetAsync(d->d_entry.p, 0, sizeof(int) * n_rows * nc * sc::kXcds, d->stream));
+                HIPCHK(hipMemsetAsync(wc.int_ctl, 0, sizeof(int) * (size_t)(1 + nc), d->stream));
                 HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kQueueWords, d->stream));
             }
             sc::launch_chain(cc, wc, launch_cfg(d), d->stream);
@@ -1368,6 +1413,8 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
             case SC_OPT_WGS_PER_CU: o.wgs_per_cu = range(0, 4); regeo = false; break;
             case SC_OPT_PROFILE: o.profile = range(0, 1); regeo = false; break;
             case SC_OPT_INTEGRAL_PASSES: o.integral_passes = range(0, 2); regeo = false; break;
+            case SC_OPT_INTEGRAL_FUSE: o.integral_fuse = range(0, 2); regeo = false; break;
+            case SC_OPT_INTEGRAL_PRE: o.integral_pre = range(0, 64); regeo = false; break;
             case SC_OPT_CHAIN_WAVES:
                 o.chain_waves = range(0, 16);
                 if (o.chain_waves != 0 && o.chain_waves != 12 && o.chain_waves != 16)

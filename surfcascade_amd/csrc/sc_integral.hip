@@ -23,11 +23,14 @@
 
 #include <cstdint>
 
+#include "sc_integral_dev.hpp"
 #include "sc_kernels.hpp"
 
 namespace sc {
 
 namespace {
+
+using namespace idev;
 
 #ifndef SC_COL_UNROLL
 #define SC_COL_UNROLL 16
@@ -37,63 +40,24 @@ constexpr int kColUnroll = SC_COL_UNROLL;  // rows per colstrip block (two block
 #define SC_COL_WAVES 1
 #endif
 
-__device__ __forceinline__ uint32_t sat_sub(uint32_t a, uint32_t b) { return a > b ? a - b : 0u; }
+#ifndef SC_RC_ROWS  // rowcarry: rows (waves) per workgroup
+#define SC_RC_ROWS 1
+#endif
+constexpr int kRcRows = SC_RC_ROWS;
 
-// The 4 gradient values of pixel (y, x) in this lane's half (T2bFilter,
-// DenseSURFFeatureExtractor.cpp:224-347), borders clamped.  Returned packed:
-// p0 = g0 | g1 << 16, p1 = g2 | g3 << 16 (strip sums stay < 2^16).
-struct Px4 {
-    uint32_t a, b, c, d;  // the four source bytes this half needs
-};
-
-__device__ __forceinline__ Px4 load_px(const uint8_t *img, int stride, int W, int H, int y, int x,
-                                       int h) {
-    const int xp = x > 0 ? x - 1 : 0, xn = x < W - 1 ? x + 1 : W - 1;
-    const uint8_t *rc = img + (long long)y * stride;
-    const uint8_t *ru = img + (long long)(y > 0 ? y - 1 : 0) * stride;
-    const uint8_t *rd = img + (long long)(y < H - 1 ? y + 1 : H - 1) * stride;
-    Px4 v;
-    if (h == 0) {  // dx: I[y][x-1], I[y][x+1]; dy: I[y-1][x], I[y+1][x]
-        v.a = rc[xp]; v.b = rc[xn]; v.c = ru[x]; v.d = rd[x];
-    } else {       // du: I[y-1][x-1], I[y+1][x+1]; dv: I[y+1][x-1], I[y-1][x+1]
-        v.a = ru[xp]; v.b = rd[xn]; v.c = rd[xp]; v.d = ru[xn];
-    }
-    return v;
-}
-
-// plane 2k = sat(Ip - In), plane 2k+1 = sat(In - Ip)  
-__device__ __forceinline__ uint2 grad_packed(const Px4 &v) {
-    // half 0: (Ip, In) = (I[y][x-1], I[y][x+1]) and (I[y-1][x], I[y+1][x])
-    // half 1: (Ip, In) = (I[y-1][x-1], I[y+1][x+1]) and (I[y+1][x-1], I[y-1][x+1])
-    const uint32_t g0 = sat_sub(v.a, v.b), g1 = sat_sub(v.b, v.a);
-    const uint32_t g2 = sat_sub(v.c, v.d), g3 = sat_sub(v.d, v.c);
-    return make_uint2(g0 | (g1 << 16), g2 | (g3 << 16));
-}
-
-// inclusive prefix sum within each 32-lane half: DPP row shifts (Hillis-
-// Steele in 16-lane rows), then row 0's / row 2's last lane broadcast into
-// rows 1 / 3 -- VALU only, no LDS round trips
-__device__ __forceinline__ uint32_t half_scan(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    return v;
-}
-
-__global__ __launch_bounds__(64) void rowcarry_kernel(RowScanArgs a) {
-    const int y = blockIdx.x, frame = blockIdx.y, lane = threadIdx.x;
+__global__ __launch_bounds__(64 * kRcRows) void rowcarry_kernel(RowScanArgs a) {
+    const int y = blockIdx.x * kRcRows + (int)(threadIdx.x >> 6), frame = blockIdx.y, lane = threadIdx.x & 63;
     const int h = lane >> 5, c = lane & 31;
     const TableGeom g = a.g;
     const int W = g.W, H = g.H, ns = (W + kStrip - 1) / kStrip;
     {   // the step's zeroed int arrays, grid-strided over the workgroups
-        const long long nt = (long long)gridDim.x * gridDim.y * 64;
-        const long long i0 = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 64 + lane;
+        const long long nt = (long long)gridDim.x * gridDim.y * 64 * kRcRows;
+        const long long i0 = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 64 * kRcRows + threadIdx.x;
 #pragma unroll
         for (int k = 0; k < 4; k++)
             for (long long i = i0; i < a.zero_n[k]; i += nt) a.zero[k][i] = 0;
     }
+    if (y >= H) return;
     const uint8_t *img = a.frames + (long long)frame * a.frame_bytes;
     float4 *tab = a.table + (long long)frame * g.frame4;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -103,7 +67,10 @@ __global__ __launch_bounds__(64) void rowcarry_kernel(RowScanArgs a) {
 
     uint4 *out = reinterpret_cast<uint4 *>(a.carry) + ((long long)frame * H + y) * ns * 2 + h;
     uint32_t run[4] = {0u, 0u, 0u, 0u};
-    constexpr int kB = 4;  // strips whose pixel loads are in flight together
+#ifndef SC_RC_KB
+#define SC_RC_KB 4
+#endif
+    constexpr int kB = SC_RC_KB;  // strips whose pixel loads are in flight together
     for (int s0 = 0; s0 < ns; s0 += kB) {
         Px4 px[kB];
 #pragma unroll
@@ -128,14 +95,6 @@ __global__ __launch_bounds__(64) void rowcarry_kernel(RowScanArgs a) {
             run[3] += ty >> 16;
         }
     }
-}
-
-// inclusive prefix sum over the whole wave: the half scan, then row 1's last
-// lane broadcast into rows 2 and 3
-__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
-    v = half_scan(v);
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return v;
 }
 
 #ifndef SC_COL_XCD
@@ -318,7 +277,7 @@ __global__ __launch_bounds__(64) void colsum4_kernel(RowScanArgs a) {
 }  // namespace
 
 void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
-    hipLaunchKernelGGL(rowcarry_kernel, dim3(a.g.H, n_frames), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(rowcarry_kernel, dim3((a.g.H + kRcRows - 1) / kRcRows, n_frames), dim3(64 * kRcRows), 0, s, a);
 }
 
 void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s) {

@@ -180,6 +180,18 @@ struct WalkArgs {
     int nseg;        // chain kernel: segments per row (8; 4 for one-frame launches)
     int seg_shift;   // chain kernel: log2(kXcds / nseg)
     unsigned long long *prof;  // chain kernel, SC_PROF_CHAIN builds: phase cycle totals (or null)
+    // Fused integral (chain kernel): colstrip's column walks of frames
+    // [int_f0, n_frames) of this launch run inside the chain kernel as a
+    // second task type; frames below int_f0 have their tables already.
+    // The walk = colstrip_kernel's (frame, 64-column strip, half) walk.
+    const uint8_t *frames;     // this launch's first frame
+    long long frame_bytes;
+    int stride;
+    const uint32_t *carry;     // rowcarry's carries of this launch's first frame
+    int int_f0;                // first frame the launch integrates
+    int int_walks;             // walks to run: (n_frames - int_f0) * walks_per_frame (0: none)
+    int walks_per_frame;       // 2 * ceil(W / 64)
+    int *int_ctl;              // [0] walk dequeue counter, [1 + f] walks finished of frame f (zeroed)
 };
 
 // Hard-negative mining (sc_mine.hip, FillNegSamples): candidate selection

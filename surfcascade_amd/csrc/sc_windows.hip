@@ -33,6 +33,7 @@
 #include <cstdint>
 
 #include "sc_device.hpp"
+#include "sc_integral_dev.hpp"
 #include "sc_kernels.hpp"
 
 namespace sc {
@@ -637,6 +638,94 @@ __host__ __device__ inline size_t chain_wave_bytes(int seg_max) {
     return (b + 15) & ~(size_t)15;  // every wave's block 16-B aligned (64-bit LDS atomics)
 }
 
+// Fused integral: colstrip_kernel's column walk (sc_integral.hip) as a task
+// of the chain kernel.  One wave per (frame, 64-column strip, channel half),
+// lane = column; the f32 column recurrence S[y+1] = S[y] + R_y in colstrip's
+// order, so the table is bit-identical.  In the chain kernel's 128-VGPR
+// budget: two blocks of kWalkRows rows of pixel loads in flight, each
+// block's strip carries loaded one row per lane and read back with
+// v_readlane.  Cells are stored write-through (buffer store with sc1: the
+// line leaves this XCD's L2), then every store is drained (vmcnt 0) before
+// lane 0 counts the walk done for its frame -- the in-launch hand-off of
+// cdna_hip_programming.md Guideline 16 (R1); the reading waves poll that
+// count and take an agent-scope acquire (chain_kernel, frame_ready).
+constexpr int kWalkRows = 8;
+static_assert((kWalkRows & (kWalkRows - 1)) == 0 && kWalkRows <= 64, "walk block");
+// SC_WALK_STORE: 1 sc1 (write-through) stores; 2 plain stores + release fence
+// at the walk's end (+0.5 % kernel time); 0 none, the tables built by the
+// separate kernels (timing ablation: the walks' cost without their stores)
+#ifndef SC_WALK_STORE
+#define SC_WALK_STORE 1
+#endif
+
+__device__ __forceinline__ void fused_walk(const CascadeArgs &a, const WalkArgs &w, int t) {
+    using namespace idev;
+    const int fi = t / w.walks_per_frame, rem = t - fi * w.walks_per_frame;
+    const int f = w.int_f0 + fi, s = rem >> 1, h = rem & 1;
+    const TableGeom g = a.g;
+    const int W = g.W, H = g.H, ns = (W + kStrip - 1) / kStrip;
+    const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const int x = s * 2 * kStrip + lane;
+    const bool live = x < W;
+    const int xs = live ? x : W - 1;  // dead lanes still join the scan with zeros
+    const uint8_t *img = w.frames + (long long)f * w.frame_bytes;
+    // the frame's table through a buffer descriptor (wave-uniform), so the
+    // 16-B stores can carry sc1 (aux 16)
+    const float4 *tab = a.table + (long long)f * g.frame4;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float4 *>(tab), (short)0, (int)(g.frame4 * 16), 0x00020000);
+    const unsigned rowb = (unsigned)g.rowp * 16u;
+    unsigned off = (unsigned)g.at(x + 1, h) * 16u + rowb;  // table row 1 of the column
+    // the exclusive carry at column 64*s is the 32-px strip 2*s's
+    const uint4 *cin = reinterpret_cast<const uint4 *>(w.carry) + (long long)f * H * ns * 2 +
+                       (long long)(2 * s) * 2 + h;
+    auto load_block = [&](int y0, Px4 (&px)[kWalkRows], uint4 &cr) {
+#pragma unroll
+        for (int k = 0; k < kWalkRows; k++) px[k] = load_px(img, w.stride, W, H, min(y0 + k, H - 1), xs, h);
+        cr = cin[(long long)min(y0 + (lane & (kWalkRows - 1)), H - 1) * ns * 2];  // lane k: row y0 + k
+    };
+    Px4 pa[kWalkRows];
+    uint4 ca;
+    load_block(0, pa, ca);
+    float S0 = 0.0f, S1 = 0.0f, S2 = 0.0f, S3 = 0.0f;  // table row 0
+    for (int y0 = 0; y0 < H; y0 += kWalkRows) {
+        Px4 pb[kWalkRows];
+        uint4 cb;
+        load_block(y0 + kWalkRows < H ? y0 + kWalkRows : y0, pb, cb);
+#pragma unroll
+        for (int k = 0; k < kWalkRows; k++) {
+            uint2 p = live ? grad_packed(pa[k]) : make_uint2(0u, 0u);
+            p.x = wave_scan(p.x);  // 16-bit channel pairs: 64 px x 255 < 2^16
+            p.y = wave_scan(p.y);
+            S0 = S0 + (float)((uint32_t)__builtin_amdgcn_readlane((int)ca.x, k) + (p.x & 0xffffu));
+            S1 = S1 + (float)((uint32_t)__builtin_amdgcn_readlane((int)ca.y, k) + (p.x >> 16));
+            S2 = S2 + (float)((uint32_t)__builtin_amdgcn_readlane((int)ca.z, k) + (p.y & 0xffffu));
+            S3 = S3 + (float)((uint32_t)__builtin_amdgcn_readlane((int)ca.w, k) + (p.y >> 16));
+            if (live && y0 + k < H) {  // rows past H: harmless extra steps, not stored
+                typedef unsigned v4u __attribute__((ext_vector_type(4)));
+                const v4u v = {__float_as_uint(S0), __float_as_uint(S1), __float_as_uint(S2), __float_as_uint(S3)};
+#if SC_WALK_STORE == 1
+                __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)off, 0, 16);  // sc1
+#elif SC_WALK_STORE == 2
+                __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)off, 0, 0);
+#else
+                if (S0 == -1.0f) __builtin_amdgcn_raw_buffer_store_b128(v, rs, (int)off, 0, 16);
+#endif
+            }
+            off += rowb;
+        }
+#pragma unroll
+        for (int k = 0; k < kWalkRows; k++) pa[k] = pb[k];
+        ca = cb;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this wave drained
+#if SC_WALK_STORE == 2
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    if (lane == 0) __hip_atomic_fetch_add(&w.int_ctl[1 + f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Lazy grid (the default detect path).  The reference evaluates only the
 // windows its adaptive-stride x chain visits (ObjDetector.cpp:185-217): after
 // a window with final score < 0.5 (or a prefilter reject) the chain skips one
@@ -672,7 +761,12 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     LevelInfo *Lv = reinterpret_cast<LevelInfo *>(smem + model_lds_bytes(a.K, LW) +
                                                   kChainWaves * chain_wave_bytes(w.row_max));
     for (int i = threadIdx.x; i < w.n_levels; i += kChainThreads) Lv[i] = w.levels[i];
-    stage_model<LW, kChainThreads>(a, smem, Wl, Bl, Ol, Rl);  // (its barrier covers Lv)
+    // fused integral: frames below *cu_rdy have complete tables this CU may
+    // read (the launch's prebuilt frames; then each frame after an sc1 poll
+    // of its walk count and an agent-scope acquire by a wave of this CU)
+    int *cu_rdy = reinterpret_cast<int *>(Lv + w.n_levels);
+    if (threadIdx.x == 0) *cu_rdy = w.int_walks > 0 ? w.int_f0 : a.n_frames;
+    stage_model<LW, kChainThreads>(a, smem, Wl, Bl, Ol, Rl);  // (its barrier covers Lv, cu_rdy)
 
     const int sa = (w.row_max + 63) & ~63, nwords = sa >> 6;  // row_max: widest segment
     unsigned char *ws = smem + model_lds_bytes(a.K, LW) + (size_t)wv * chain_wave_bytes(w.row_max);
@@ -710,12 +804,51 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     unsigned long long t_last = __builtin_amdgcn_s_memtime();
 #endif
 
+    // Fused integral: the last wave of every workgroup first runs column
+    // walks (fused_walk) until none is left, then joins the chain work.  One
+    // walker per workgroup: whichever workgroups are resident, the walks of
+    // every frame progress, so no wave waits on a frame forever.
+    if (w.int_walks > 0 && wv == kChainWaves - 1) {
+        __builtin_amdgcn_s_setprio(2);  // latency-bound: issue ahead of the gathers
+        for (;;) {
+            int t = 0;
+            if (lane_id<RM>() == 0) t = atomicAdd(&w.int_ctl[0], 1);
+            t = __builtin_amdgcn_readfirstlane(t);
+            if (t >= w.int_walks) break;
+#ifndef SC_NO_WALK
+            fused_walk(a, w, t);
+#endif
+        }
+        __builtin_amdgcn_s_setprio(0);
+    }
+    // Frame fr's table is complete and this CU may read it (Guideline 16:
+    // the acquire invalidates the CU's L1; the LDS word, raised after the
+    // acquire's wait, orders the CU's other waves after it)
+    auto frame_ready = [&](int fr) -> bool {
+        int c = __builtin_amdgcn_readfirstlane(__hip_atomic_load(cu_rdy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (fr < c) return true;
+        const int c0 = c;
+        while (c < a.n_frames) {
+            int v = 0;
+            if (lane_id<RM>() == 0)
+                v = __hip_atomic_load(&w.int_ctl[1 + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__builtin_amdgcn_readfirstlane(v) < w.walks_per_frame) break;
+            c++;
+        }
+        if (c > c0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (lane_id<RM>() == 0) __hip_atomic_fetch_max(cu_rdy, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        return fr < c;
+    };
+
     // per-slot task state (wave-uniform)
     int st[kSlots], tq[kSlots], tt[kSlots], r[kSlots], j0[kSlots], nseg[kSlots];
     int frame[kSlots], level[kSlots], ys[kSlots];
     unsigned nvis[kSlots];
 #pragma unroll
-    for (int sl = 0; sl < kSlots; sl++) st[sl] = 0;  // 0 empty, 1 waiting for entry, 2 active
+    for (int sl = 0; sl < kSlots; sl++) st[sl] = 0;  // 0 empty, 1 waiting for entry, 2 active, 3 waiting for the frame's table
 
 #ifndef SC_FILL_K  // launch fill: segment-0 tasks per wave = SC_FILL_K * s / SC_FILL_DEN
 #define SC_FILL_K 1
@@ -803,8 +936,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     j0[sl] = min(nx, qq * nxs);
                     nseg[sl] = min(nx, j0[sl] + nxs) - j0[sl];
                     nvis[sl] = 0;
-                    st[sl] = 1;
-                    if (qq == 0 || SC_ABL_NOWAIT) start(sl, j0[sl]);  // (segment 0 enters at 0)
+                    st[sl] = 3;  // the poll below checks the frame, then starts segment 0
                 }
                 SC_PROF(c_deq);
             }
@@ -812,6 +944,12 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         {   // poll every waiting slot once, the loads in flight together; a lost
             // hand-off must not hang the GPU (watchdog below)
             int e[kSlots];
+#pragma unroll
+            for (int sl = 0; sl < kSlots; sl++)
+                if (st[sl] == 3 && frame_ready(frame[sl])) {
+                    st[sl] = 1;
+                    if (tq[sl] == 0 || SC_ABL_NOWAIT) start(sl, j0[sl]);  // (segment 0 enters at 0)
+                }
 #pragma unroll
             for (int sl = 0; sl < kSlots; sl++) {
                 e[sl] = 0;
@@ -824,7 +962,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                 const int es = __builtin_amdgcn_readfirstlane(e[sl]);
                 if (st[sl] == 1 && es) start(sl, es - 1);
                 n_active += st[sl] == 2;
-                n_wait += st[sl] == 1;
+                n_wait += st[sl] == 1 || st[sl] == 3;
             }
             SC_PROF(c_poll);
         }
@@ -838,7 +976,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             if (++idle == (1u << 24)) {  // a lost hand-off must not hang the GPU
 #pragma unroll
                 for (int sl = 0; sl < kSlots; sl++)
-                    if (st[sl] == 1) {
+                    if (st[sl] == 1 || st[sl] == 3) {
                         if (lane_id<RM>() == 0) atomicAdd(w.err, 1);
                         start(sl, j0[sl]);
                     }
@@ -1094,7 +1232,7 @@ void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s) {
 }
 
 int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hipStream_t s) {
-    auto scratch = [&](int nw) { return nw * chain_wave_bytes(w.row_max) + w.n_levels * sizeof(LevelInfo); };
+    auto scratch = [&](int nw) { return nw * chain_wave_bytes(w.row_max) + w.n_levels * sizeof(LevelInfo) + 16; };
     const size_t kLds = 160 * 1024;
     // 16 waves with the weights in LDS when they fit and a frame's table sits
     // comfortably in the 256 MiB Infinity Cache; else 12 (weights in LDS when
@@ -1104,8 +1242,10 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hi
     // (levels 13-23 alone: 106 % of the measured gather ceiling, +12 % at 16
     // waves); a 4K frame's 265 MB table leaves the Infinity Cache (C4: +8 %
     // at 16 waves).  C2 as a whole: -2.7 % (profiles/r3/g3).
+    // One-frame launches (the latency path): 12 (0.656 vs 0.673 ms per 1080p
+    // frame, profiles/r3/g12), the hand-off fill and drain dominate them.
     const bool fabric_bound = a.g.frame4 * 16 > (128ll << 20);
-    int nw = !fabric_bound && model_lds_bytes(a.K, true) + scratch(16) <= kLds ? 16 : 12;
+    int nw = !fabric_bound && a.n_frames > 1 && model_lds_bytes(a.K, true) + scratch(16) <= kLds ? 16 : 12;
     if (c.chain_waves == 12 || (c.chain_waves == 16 && model_lds_bytes(a.K, false) + scratch(16) <= kLds))
         nw = c.chain_waves;  // SC_OPT_CHAIN_WAVES
     bool lw = model_lds_bytes(a.K, true) + scratch(nw) <= kLds;
@@ -1136,7 +1276,7 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hi
 }
 
 size_t chain_lds_bytes(int K, int row_max, int n_levels) {  // smallest variant (12 waves, weights via caches)
-    return model_lds_bytes(K, false) + 12 * chain_wave_bytes(row_max) + n_levels * sizeof(LevelInfo);
+    return model_lds_bytes(K, false) + 12 * chain_wave_bytes(row_max) + n_levels * sizeof(LevelInfo) + 16;
 }
 
 size_t cascade_lds_bytes(int K, int strip_max, int band_rows) {  // smallest variant

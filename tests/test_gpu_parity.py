@@ -190,6 +190,37 @@ def test_integral_batch_frames(sc, oracle, n):
         assert T.view(np.uint32).tobytes() == oracle.integral(frames[k]).view(np.uint32).tobytes()
 
 
+@pytest.mark.parametrize("n,opts", [(2, {"integral_fuse": 2}), (5, {"integral_pre": 2}),
+                                    (7, {"chain_chunk": 3, "integral_fuse": 2}), (4, {}),
+                                    (4, {"integral_fuse": 1}), (6, {"integral_pre": 1, "chain_waves": 12})])
+def test_fused_integral(sc, oracle, face_cascade, n, opts):
+    """The integral's column walks inside the chain kernel (SC_OPT_INTEGRAL_FUSE,
+    the default from 4 frames per launch): every frame's table, evaluated
+    windows, visited set and detections are the oracle's -- with 1 or 2
+    frames integrated ahead, several launches (chain_chunk 3: 3 + 3 + 1
+    frames), both chain-kernel widths and fusion off.  Two batches through one
+    detector, so the second reads table lines the first left in the caches."""
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=5)).set_options(**opts)
+    det.set_debug(True)
+    params = oracle.Params(n_levels=5)
+    for rep in range(2):
+        frames = np.stack([_frame(641, 483, 3000 + 37 * rep + k) for k in range(n)])
+        batch = det.detect_batch(frames)
+        layout, _ = oracle.grid_layout(641, 483, params)
+        for k in range(n):
+            T = oracle.integral(frames[k])
+            assert det.dump_integral(641, 483, frame=k).view(np.uint32).tobytes() == T.view(np.uint32).tobytes()
+            p, s, v = det.dump_grid(frame=k)
+            rp, rs = oracle.eval_grid(T, face_cascade, params)
+            ev = p != -2
+            np.testing.assert_array_equal(p[ev], rp[ev])
+            assert s[ev].view(np.uint32).tobytes() == rs[ev].view(np.uint32).tobytes()
+            rv, _ = oracle.walk_grid(rp, rs, layout, face_cascade.n_stages, params.stride_score)
+            np.testing.assert_array_equal(v, rv)
+            ref, _ = oracle.detect(T, face_cascade, params)
+            assert _det_set(batch[k]) == _det_set(ref)
+
+
 @pytest.mark.parametrize("segs", ["1", "2", "8"])
 def test_chain_segments_per_row(sc, oracle, face_cascade, segs):
     """A single frame with other segment counts than its default 4: the
