@@ -154,7 +154,7 @@ struct sc_detector {
     int table_frames = 0;
     DevBuf<sc_det_record> d_out;
     DevBuf<int> d_counters;
-    DevBuf<unsigned> d_visited;  // per (frame, row): windows the x chain visited
+    DevBuf<unsigned> d_visited;  // [frame][row] words whose sum is the windows the x chain visited
     DevBuf<int> d_queues;       // per-XCD task counters of the cascade kernel
     DevBuf<int> d_entry;        // chain kernel: per (row, segment) chain entry + 1
     DevBuf<unsigned long long> d_prof;  // chain kernel phase cycles (SC_PROF_CHAIN builds)

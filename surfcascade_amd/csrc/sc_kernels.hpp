@@ -171,7 +171,7 @@ struct WalkArgs {
     sc_det_record *out;
     int capacity;
     int *counters;  // [0] total, [1+f] per frame
-    unsigned *row_visited;  // [frame][row] windows the x chain visited
+    unsigned *row_visited;  // [frame][row] words; their sum = windows the x chain visited (walk kernel: per row)
     uint8_t *dbg_v;  // optional [frame][grid] visited flags
     int row_max;     // chain kernel: most windows in one row segment (LDS sizing)
     int *entry;      // chain kernel: [frame*rows][kXcds] chain entry + 1 per segment (zeroed)

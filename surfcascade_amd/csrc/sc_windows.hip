@@ -846,7 +846,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     // per-slot task state (wave-uniform)
     int st[kSlots], tq[kSlots], tt[kSlots], r[kSlots], j0[kSlots], nseg[kSlots];
     int frame[kSlots], level[kSlots], ys[kSlots];
-    unsigned nvis[kSlots];
+    unsigned vtot = 0;  // windows this wave's chains visited (summed into row_visited at the end)
 #pragma unroll
     for (int sl = 0; sl < kSlots; sl++) st[sl] = 0;  // 0 empty, 1 waiting for entry, 2 active, 3 waiting for the frame's table
 
@@ -903,7 +903,6 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             if (tq[sl] + 1 < nsg)
                 __hip_atomic_store(&w.entry[(long long)tt[sl] * nsg + tq[sl] + 1], pos + 1,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (nvis[sl]) atomicAdd(&w.row_visited[tt[sl]], nvis[sl]);
         }
         st[sl] = 0;
     };
@@ -935,7 +934,6 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     ys[sl] = rd.y;
                     j0[sl] = min(nx, qq * nxs);
                     nseg[sl] = min(nx, j0[sl] + nxs) - j0[sl];
-                    nvis[sl] = 0;
                     st[sl] = 3;  // the poll below checks the frame, then starts segment 0
                 }
                 SC_PROF(c_deq);
@@ -1040,7 +1038,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             for (int sl = 0; sl < kSlots; sl++) {
                 int *pk = park + sl * 10;
                 pk[0] = st[sl]; pk[1] = tq[sl]; pk[2] = tt[sl]; pk[3] = r[sl]; pk[4] = j0[sl];
-                pk[5] = nseg[sl]; pk[6] = frame[sl]; pk[7] = level[sl]; pk[8] = (int)nvis[sl];
+                pk[5] = nseg[sl]; pk[6] = frame[sl]; pk[7] = level[sl];
                 pk[9] = ys[sl];
             }
         }
@@ -1070,7 +1068,6 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             nseg[sl] = __builtin_amdgcn_readfirstlane(pk[5]);
             frame[sl] = __builtin_amdgcn_readfirstlane(pk[6]);
             level[sl] = __builtin_amdgcn_readfirstlane(pk[7]);
-            nvis[sl] = (unsigned)__builtin_amdgcn_readfirstlane(pk[8]);
             ys[sl] = __builtin_amdgcn_readfirstlane(pk[9]);
         }
 
@@ -1170,7 +1167,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     if (lim < 64) rr = (c << 6) + (63 - __builtin_clzll(path)) + 2;
                     else rr = ((c + 1) << 6) + (b & 1);
                 }
-                nvis[sl] += __popcll(vis);
+                vtot += __popcll(vis);
                 if (w.dbg_v && ((vis >> lane_id<RM>()) & 1ull)) w.dbg_v[gi0 + (c << 6) + lane_id<RM>()] = 1;
                 if (f < qg || rr >= ns) break;
             }
@@ -1180,6 +1177,11 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         wave_sync();
         SC_PROF(c_merge);
     }
+    // the visited count: only its sum is read (SC_INFO_VISITED), so one add
+    // per wave instead of one returning-free atomic per task, spread over the
+    // launch's words (the poll after a task's end waits for its atomics)
+    if (vtot && lane_id<RM>() == 0)
+        atomicAdd(&w.row_visited[(blockIdx.x * kChainWaves + wv) % (w.n_rows * a.n_frames)], vtot);
 #if SC_PROF_CHAIN
     if (w.prof && lane_id<RM>() == 0) {
         atomicAdd(&w.prof[0], c_idle);
