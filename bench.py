@@ -386,6 +386,7 @@ def main():
     det.set_timing(False)
     kt = det.get_timing()
     visited = det.info("visited")
+    fused_frames = det.info("fused_frames")  # (before the latency / host legs replace the last call)
     if dist is None:
         check_capacity()
     # single-frame latency (C2 names "1080p frame"): batch-1 steps, device-resident
@@ -429,10 +430,15 @@ def main():
         value = windows / dt
         # roofline of the dominant kernel (windows): its compulsory bytes per
         # launch = the integral table read once (32 B x (W+1)(H+1) per frame)
+        # and, for the frames whose integral ran inside it (fused column
+        # walks), the table written once, the frame read and its strip carries
         tab_bytes = 32 * (W + 1) * (H + 1)
         ms_win, n_win = kt["windows"]
         avg_win_s = ms_win / 1e3 / max(n_win, 1)
-        achieved = tab_bytes * B / max(avg_win_s, 1e-12) / 1e9
+        launches = max(n_win // max(args.steps, 1), 1)  # chain launches per step
+        fused = fused_frames / launches
+        win_bytes = tab_bytes * B + fused * (tab_bytes + W * H + H * ((W + 31) // 32) * 32)
+        achieved = win_bytes / max(avg_win_s, 1e-12) / 1e9
         # whole pipeline (SURVEY.md 8d per-unit figure: W*H + 64 (W+1)(H+1) per frame)
         pipe_bytes = W * H + 64 * (W + 1) * (H + 1)
         pipe_s = max(sum(v[0] for v in kt.values()) / 1e3 / max(n_win, 1), 1e-12)
@@ -461,8 +467,8 @@ def main():
                        "levels": args.levels,
                        "parallelism": ("grid-row-sharded x%d" if grid_shard else "frame-sharded dp%d")
                        % world},
-            "roofline": roofline(achieved, traffic, valu_insts, avg_win_s, tab_bytes * B, pipe_bytes * B,
-                                 pipe_s, pmc, opts),
+            "roofline": roofline(achieved, traffic, valu_insts, avg_win_s, win_bytes, pipe_bytes * B,
+                                 pipe_s, pmc, opts, fused),
             "kernel_ms_per_launch": {k: v[0] / max(v[1], 1) for k, v in kt.items()},
             "visited_windows_last_step": visited,
             "detections_last_step": total_det,
@@ -510,12 +516,14 @@ def pmc_for(args, B, W):
     return {}
 
 
-def roofline(achieved, traffic, valu_insts, avg_win_s, bytes_launch, pipe_bytes, pipe_s, pmc, opts):
+def roofline(achieved, traffic, valu_insts, avg_win_s, bytes_launch, pipe_bytes, pipe_s, pmc, opts,
+             fused=0):
     r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
          "kernel": "cascade_kernel" if opts.get("full_grid") else "chain_kernel",
          "avg_launch_ms": avg_win_s * 1e3,
          "bytes_per_launch": bytes_launch,
+         "fused_integral_frames_per_launch": fused,
          "pipeline_achieved": pipe_bytes / pipe_s / 1e9,
          "pipeline_frac": pipe_bytes / pipe_s / 1e9 / HBM_PEAK_GBS,
          # beyond-L2 bytes per compulsory byte: re-reads of the table

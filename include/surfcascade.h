@@ -189,6 +189,8 @@ int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, 
 #define SC_INFO_ROWS 3          /* (level, y) rows per frame                 */
 #define SC_INFO_TABLE_PITCH 4   /* integral-table row pitch in cells         */
 #define SC_INFO_VISITED 5       /* windows the adaptive stride visited (last) */
+#define SC_INFO_FUSED_FRAMES 6  /* frames of the last call whose integral      */
+                                /* column walks ran inside the chain kernel    */
 int sc_detector_info(sc_detector *d, int what, int64_t *value);
 
 /* ---- tuning and test options ---------------------------------------------
@@ -227,8 +229,9 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
                               /* frame's table is <= 128 MiB and the launch    */
                               /* has 2+ frames), 12, 16                        */
 #define SC_OPT_INTEGRAL_FUSE 18 /* integral column walks inside the chain      */
-                              /* kernel: 0 auto (from 4 frames per launch),    */
-                              /* 1 never, 2 whenever a launch has 2+ frames    */
+                              /* kernel: 0 auto (from 4 frames per launch, for */
+                              /* tables <= 128 MiB), 1 never, 2 whenever a     */
+                              /* launch has 2+ frames                          */
 #define SC_OPT_INTEGRAL_PRE 19 /* fused: frames per launch integrated before   */
                               /* the chain kernel (0: default 2)               */
 int sc_detector_set_option(sc_detector *d, int option, int64_t value);

@@ -165,6 +165,7 @@ struct sc_detector {
     bool debug = false;
     DevBuf<uint8_t> d_dbg_v;    // per grid window: visited by the x chain
     int last_frames = 0;
+    int last_fused = 0;  // frames of the last call integrated inside the chain kernel
     // timing
     bool timing = false;
     struct Pending {
@@ -616,11 +617,16 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     // frame 0, 13.63 vs 13.74 ms chain kernel at C2, profiles/r3/g10), the
     // column walks of the others run inside the chain kernel as a second
     // task type, overlapping the gathers.  Auto: from
-    // 4 frames per launch, where colstrip would be the integral's column pass.
+    // 4 frames per launch, where colstrip would be the integral's column pass,
+    // and for tables that fit the Infinity Cache: a 4K frame's 265 MB table
+    // leaves it, its chain kernel already gathers from HBM beyond the
+    // fabric's rate and the walks' stores cost more than they hide (C4: 26.09
+    // vs 25.88 ms per 8-frame step, profiles/r3/g21).
     const int pre = d->opt.integral_pre > 0 ? d->opt.integral_pre : 2;
     const int fuse_from = d->opt.integral_fuse == 2 ? 2 : 4;
     const bool fuse = chain && d->opt.integral_fuse != 1 && std::min(chunk, n) >= fuse_from &&
-                      std::min(chunk, n) > pre;
+                      std::min(chunk, n) > pre &&
+                      (d->opt.integral_fuse == 2 || g.tg.frame4 * 16 <= (128ll << 20));
 
     sc::RowScanArgs ra{d_frames, (long long)H * stride, stride, d->d_table.p, g.tg, d->d_carry.p, {}, {}};
     // zeroed by rowcarry (stream order: before every kernel that uses them):
@@ -669,6 +675,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     timed_end(d, SC_KERNEL_COLSCAN, e0);
 
     d->last_frames = n;
+    d->last_fused = 0;
     if (g.rows.empty()) return;
 
     sc::CascadeArgs ca{};
@@ -748,6 +755,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
                 wc.int_f0 = pre;
                 wc.walks_per_frame = 2 * ((W + 2 * sc::kStrip - 1) / (2 * sc::kStrip));
                 wc.int_walks = (nc - pre) * wc.walks_per_frame;
+                d->last_fused += nc - pre;
             }
             wc.frame0 = f0;
             wc.nseg = segs_for(nc);
@@ -1357,6 +1365,7 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value) {
         case SC_INFO_GRID_WINDOWS: *value = d->geo.grid; break;
         case SC_INFO_ROWS: *value = (int64_t)d->geo.rows.size(); break;
         case SC_INFO_TABLE_PITCH: *value = d->geo.tg.rowp; break;
+        case SC_INFO_FUSED_FRAMES: *value = d->last_fused; break;
         case SC_INFO_VISITED: {  // sum of the walk kernel's per-row counts
             return guarded([&] {
                 HIPCHK(hipSetDevice(d->device));

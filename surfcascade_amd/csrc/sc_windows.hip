@@ -808,7 +808,10 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     // walks (fused_walk) until none is left, then joins the chain work.  One
     // walker per workgroup: whichever workgroups are resident, the walks of
     // every frame progress, so no wave waits on a frame forever.
-    if (w.int_walks > 0 && wv == kChainWaves - 1) {
+#ifndef SC_WALKERS  // walking waves per workgroup (1 measured best of 1/8, 1/4, 1/2, 1, 2: profiles/r3/g18-19)
+#define SC_WALKERS 1
+#endif
+    if (w.int_walks > 0 && wv >= kChainWaves - SC_WALKERS) {
         __builtin_amdgcn_s_setprio(2);  // latency-bound: issue ahead of the gathers
         for (;;) {
             int t = 0;

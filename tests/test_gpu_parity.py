@@ -505,6 +505,26 @@ def test_integral_extreme_content(sc, oracle, kind, passes):
     assert T.view(np.uint32).tobytes() == ref.view(np.uint32).tobytes()
 
 
+@pytest.mark.parametrize("layout", ["0", "1"])
+@pytest.mark.parametrize("W,H", [(1920, 1080), (257, 131)])
+def test_integral_fused_extreme_content(sc, oracle, layout, W, H):
+    """The fused integral (column walks inside the chain kernel: frames 1.. of
+    the launch with integral_pre 1) on the extreme contents of
+    test_integral_extreme_content, at 1080p and at a ragged size whose last
+    64-column strip is 1 px wide; both table layouts; every frame bit-exact."""
+    yy, xx = np.mgrid[0:H, 0:W]
+    frames = np.stack([np.random.default_rng(8).integers(0, 256, (H, W)), ((xx + yy) & 1) * 255,
+                       np.random.default_rng(7).integers(0, 256, (H, W)), np.zeros((H, W)),
+                       np.full((H, W), 255), (xx & 1) * 255]).astype(np.uint8)
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1)).set_options(
+        table_layout=int(layout), integral_fuse=2, integral_pre=1)
+    det.set_debug(True)
+    det.detect_batch(frames)
+    for k in range(len(frames)):
+        T = det.dump_integral(W, H, frame=k)
+        assert T.view(np.uint32).tobytes() == oracle.integral(frames[k]).view(np.uint32).tobytes(), k
+
+
 @pytest.mark.parametrize("kind", ["checker", "noise"])
 def test_grid_parity_extreme_content(sc, oracle, face_cascade, kind):
     """Per-window bits, visited set and detections on frames where every
