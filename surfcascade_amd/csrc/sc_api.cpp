@@ -994,26 +994,32 @@ int guarded(F &&f) {
 // =========================================================================
 // C ABI
 // =========================================================================
-// Host frames (any row stride) -> d->d_frames, packed w x h per frame: each
-// frame is copied into the pinned staging buffer and its DMA queued at once,
-// so the host copy of frame f+1 overlaps the transfer of frame f.  The
-// caller's stream synchronisation at the end of the call covers the staging
-// buffer's reuse by the next call.
-static void upload_frames(sc_detector *d, const uint8_t *const *frames, int n, int w, int h, int stride) {
-    const size_t fb = (size_t)w * h;
+// Host frames (any row stride) -> d->d_frames, w x h per frame at a row
+// pitch rounded up to 4 bytes (rowcarry4's dword loads; the pad bytes are
+// never part of a result), returned: each frame is copied into the pinned
+// staging buffer and its DMA queued at once, so the host copy of frame f+1
+// overlaps the transfer of frame f.  The caller's stream synchronisation at
+// the end of the call covers the staging buffer's reuse by the next call.
+static int upload_frames(sc_detector *d, const uint8_t *const *frames, int n, int w, int h, int stride) {
+    const int pitch = (w + 3) & ~3;
+    const size_t fb = (size_t)pitch * h;
     HIPCHK(hipStreamSynchronize(d->stream));  // no earlier transfer still reads the staging buffer
     d->d_frames.ensure(fb * n);
     d->h_stage.ensure(fb * n);
     for (int f = 0; f < n; f++) {
         if (!frames[f]) throw Error{SC_ERR_INVALID, "null frame pointer"};
         uint8_t *dst = d->h_stage.p + fb * f;
-        if (stride == w) {
+        if (stride == w && w == pitch) {  // (a caller's last row may end at w: copy no pad)
             std::memcpy(dst, frames[f], fb);
         } else {
-            for (int y = 0; y < h; y++) std::memcpy(dst + (size_t)y * w, frames[f] + (size_t)y * stride, w);
+            for (int y = 0; y < h; y++) {
+                std::memcpy(dst + (size_t)y * pitch, frames[f] + (size_t)y * stride, w);
+                if (pitch > w) std::memset(dst + (size_t)y * pitch + w, 0, pitch - w);
+            }
         }
         HIPCHK(hipMemcpyAsync(d->d_frames.p + fb * f, dst, fb, hipMemcpyHostToDevice, d->stream));
     }
+    return pitch;
 }
 
 extern "C" {
@@ -1288,8 +1294,8 @@ int sc_mine_batch(sc_detector *d, const uint8_t *const *frames, int n, int w, in
         if (!d || !frames || n <= 0) throw Error{SC_ERR_INVALID, "bad arguments"};
         if (w < 2 || h < 2 || stride < w) throw Error{SC_ERR_INVALID, "bad frame geometry"};
         HIPCHK(hipSetDevice(d->device));
-        upload_frames(d, frames, n, w, h, stride);
-        return mine_sync(d, d->d_frames.p, n, w, h, w, wins, features, capacity, n_out);
+        const int pitch = upload_frames(d, frames, n, w, h, stride);
+        return mine_sync(d, d->d_frames.p, n, w, h, pitch, wins, features, capacity, n_out);
     });
 }
 
@@ -1322,8 +1328,8 @@ int sc_detect_batch(sc_detector *d, const uint8_t *const *frames, int n, int w, 
         if (!d || !frames || n <= 0) throw Error{SC_ERR_INVALID, "bad arguments"};
         if (w < 2 || h < 2 || stride < w) throw Error{SC_ERR_INVALID, "bad frame geometry"};
         HIPCHK(hipSetDevice(d->device));
-        upload_frames(d, frames, n, w, h, stride);
-        return detect_device_sync(d, d->d_frames.p, n, w, h, w, out, capacity, n_out);
+        const int pitch = upload_frames(d, frames, n, w, h, stride);
+        return detect_device_sync(d, d->d_frames.p, n, w, h, pitch, out, capacity, n_out);
     });
 }
 

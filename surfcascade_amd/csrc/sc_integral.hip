@@ -97,6 +97,114 @@ __global__ __launch_bounds__(64 * kRcRows) void rowcarry_kernel(RowScanArgs a) {
     }
 }
 
+// rowcarry with dword pixel loads (frames whose rows start 4-B aligned):
+// one wave per (row, frame), 4 columns per lane, 256 columns per pass.  The
+// byte-load form issues 4 loads per lane per 32-column strip and is bound by
+// the texture-address unit (TA busy ~80 % of its time: one instruction costs
+// the same whatever it moves); here a pass is 3 dword loads per lane (rows
+// y-1, y, y+1), the x-1 / x+4 neighbours come from the adjacent lanes by DPP
+// wave shifts (the pass's edges from the neighbouring passes), and the 8
+// channel sums of a lane's 4 columns go through one wave scan per channel
+// pair.  Same gradients, same exact u32 strip carries as rowcarry_kernel.
+__device__ __forceinline__ uint32_t byte_of(unsigned long long w, int i) {
+    return (uint32_t)(w >> (8 * i)) & 0xffu;
+}
+
+__global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
+    const int y = blockIdx.x, frame = blockIdx.y, lane = threadIdx.x;
+    const TableGeom g = a.g;
+    const int W = g.W, H = g.H, ns = (W + kStrip - 1) / kStrip;
+    {   // the step's zeroed int arrays, grid-strided over the workgroups
+        const long long nt = (long long)gridDim.x * gridDim.y * 64;
+        const long long i0 = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            for (long long i = i0; i < a.zero_n[k]; i += nt) a.zero[k][i] = 0;
+    }
+    const uint8_t *img = a.frames + (long long)frame * a.frame_bytes;
+    float4 *tab = a.table + (long long)frame * g.frame4;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (y == 0)  // table row 0 is all zeros
+        for (int i = lane; i < g.rowp; i += 64) tab[i] = z4;
+    if (lane < 2) tab[(long long)(y + 1) * g.rowp + lane * g.hs] = z4;  // column 0
+
+    const uint32_t *ru = reinterpret_cast<const uint32_t *>(img + (long long)(y > 0 ? y - 1 : 0) * a.stride);
+    const uint32_t *rc = reinterpret_cast<const uint32_t *>(img + (long long)y * a.stride);
+    const uint32_t *rd = reinterpret_cast<const uint32_t *>(img + (long long)(y < H - 1 ? y + 1 : H - 1) * a.stride);
+    uint4 *out = reinterpret_cast<uint4 *>(a.carry) + ((long long)frame * H + y) * ns * 2;
+    const int np = (W + 255) / 256;
+    // a pass's dwords (rows u, c, d), loaded one pass ahead
+    auto load = [&](int p, uint32_t &u, uint32_t &c, uint32_t &d) {
+        const int x0 = p * 256 + 4 * lane;
+        u = c = d = 0u;
+        if (p < np && x0 < W) {  // (stride % 4 == 0: the dword stays inside the row's pitch)
+            u = ru[x0 >> 2];
+            c = rc[x0 >> 2];
+            d = rd[x0 >> 2];
+        }
+    };
+    uint32_t u0, c0, d0;
+    load(0, u0, c0, d0);
+    // the byte left of the pass (x0 - 1 of lane 0): the previous pass's last;
+    // x = 0 clamps to itself
+    uint32_t lu = u0 & 0xffu, lc = c0 & 0xffu, ld = d0 & 0xffu;
+    uint32_t run[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    for (int p = 0; p < np; p++) {
+        uint32_t u1, c1, d1;
+        load(p + 1, u1, c1, d1);
+        // the byte right of the pass (x0 + 4 of lane 63): the next pass's first
+        const uint32_t nu = (uint32_t)__builtin_amdgcn_readlane((int)u1, 0) & 0xffu;
+        const uint32_t nc = (uint32_t)__builtin_amdgcn_readlane((int)c1, 0) & 0xffu;
+        const uint32_t nd = (uint32_t)__builtin_amdgcn_readlane((int)d1, 0) & 0xffu;
+        // bytes x0-1 .. x0+4 of each row (lanes l-1 / l+1 by wave_shr / wave_shl)
+        auto window = [&](uint32_t v, uint32_t left, uint32_t right) -> unsigned long long {
+            const uint32_t l = (uint32_t)__builtin_amdgcn_update_dpp((int)(left << 24), (int)v, 0x138, 0xf, 0xf, false) >> 24;
+            const uint32_t r = (uint32_t)__builtin_amdgcn_update_dpp((int)right, (int)v, 0x130, 0xf, 0xf, false) & 0xffu;
+            return ((unsigned long long)r << 40) | ((unsigned long long)v << 8) | l;
+        };
+        const unsigned long long U = window(u0, lu, nu), C = window(c0, lc, nc), D = window(d0, ld, nd);
+        const int x0 = p * 256 + 4 * lane;
+        uint32_t G[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int x = x0 + j;
+            if (x < W) {
+                const int il = j, im = j + 1, ir = x + 1 < W ? j + 2 : j + 1;  // x = W-1: x+1 clamps to x
+                // half 0: (C[x-1], C[x+1]), (U[x], D[x]); half 1: (U[x-1], D[x+1]), (D[x-1], U[x+1])
+                const uint32_t a0 = byte_of(C, il), b0 = byte_of(C, ir), c0_ = byte_of(U, im), d0_ = byte_of(D, im);
+                const uint32_t a1 = byte_of(U, il), b1 = byte_of(D, ir), c1_ = byte_of(D, il), d1_ = byte_of(U, ir);
+                G[0] += sat_sub(a0, b0); G[1] += sat_sub(b0, a0); G[2] += sat_sub(c0_, d0_); G[3] += sat_sub(d0_, c0_);
+                G[4] += sat_sub(a1, b1); G[5] += sat_sub(b1, a1); G[6] += sat_sub(c1_, d1_); G[7] += sat_sub(d1_, c1_);
+            }
+        }
+        // 16-bit channel pairs: a pass's prefix stays < 64 x 4 x 255 < 2^16
+        uint32_t q[4] = {G[0] | (G[1] << 16), G[2] | (G[3] << 16), G[4] | (G[5] << 16), G[6] | (G[7] << 16)};
+        uint32_t e[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t incl = wave_scan(q[k]);
+            e[k] = incl - q[k];  // exclusive: the columns of the pass left of this lane
+            q[k] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);  // the pass's totals
+        }
+        const int s = p * 8 + (lane >> 3);  // 32-column strip starting at this lane (lane % 8 == 0)
+        if ((lane & 7) == 0 && s < ns) {
+            out[(long long)s * 2] = make_uint4(run[0] + (e[0] & 0xffffu), run[1] + (e[0] >> 16),
+                                               run[2] + (e[1] & 0xffffu), run[3] + (e[1] >> 16));
+            out[(long long)s * 2 + 1] = make_uint4(run[4] + (e[2] & 0xffffu), run[5] + (e[2] >> 16),
+                                                   run[6] + (e[3] & 0xffffu), run[7] + (e[3] >> 16));
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            run[2 * k] += q[k] & 0xffffu;
+            run[2 * k + 1] += q[k] >> 16;
+        }
+        lu = (uint32_t)__builtin_amdgcn_readlane((int)u0, 63) >> 24;
+        lc = (uint32_t)__builtin_amdgcn_readlane((int)c0, 63) >> 24;
+        ld = (uint32_t)__builtin_amdgcn_readlane((int)d0, 63) >> 24;
+        u0 = u1; c0 = c1; d0 = d1;
+    }
+}
+
 #ifndef SC_COL_XCD
 #define SC_COL_XCD 1
 #endif
@@ -276,8 +384,15 @@ __global__ __launch_bounds__(64) void colsum4_kernel(RowScanArgs a) {
 
 }  // namespace
 
+#ifndef SC_RC_DWORD  // rowcarry4 (dword loads) when the rows start 4-B aligned
+#define SC_RC_DWORD 1
+#endif
 void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
-    hipLaunchKernelGGL(rowcarry_kernel, dim3((a.g.H + kRcRows - 1) / kRcRows, n_frames), dim3(64 * kRcRows), 0, s, a);
+    const bool aligned = ((uintptr_t)a.frames & 3u) == 0 && (a.stride & 3) == 0;
+    if (SC_RC_DWORD && aligned)
+        hipLaunchKernelGGL(rowcarry4_kernel, dim3(a.g.H, n_frames), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL(rowcarry_kernel, dim3((a.g.H + kRcRows - 1) / kRcRows, n_frames), dim3(64 * kRcRows), 0, s, a);
 }
 
 void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s) {

@@ -341,6 +341,28 @@ def test_strided_frames(sc, oracle, face_cascade):
         det.detect_device(torch.from_numpy(wide).to("cuda:0").transpose(1, 2))
 
 
+@pytest.mark.parametrize("pitch,off", [(644, 0), (643, 0), (700, 30), (700, 32)])
+def test_integral_device_pitch(sc, oracle, pitch, off):
+    """Device frames whose rows start 4-B aligned (pitch 644 / 700 at column
+    offset 0 / 32) take the dword-load rowcarry4 kernel, the others (pitch
+    643, offset 30) the byte-load rowcarry; a 641-px row ends inside a dword.
+    Every frame's table is bit-exact either way (3 frames: two-pass column
+    pass; 5 frames: colstrip or the fused walks)."""
+    import torch
+    W, H = 641, 301
+    rng = np.random.default_rng(pitch + off)
+    for n in (3, 5):
+        buf = rng.integers(0, 256, (n, H, pitch), dtype=np.uint8)
+        view = buf[:, :, off:off + W]
+        det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=2))
+        det.set_debug(True)
+        det.detect_device(torch.from_numpy(buf).to("cuda:0")[:, :, off:off + W])
+        for k in range(n):
+            T = det.dump_integral(W, H, frame=k)
+            ref = oracle.integral(np.ascontiguousarray(view[k]))
+            assert T.view(np.uint32).tobytes() == ref.view(np.uint32).tobytes(), (n, k)
+
+
 def test_capacity_error_reports_count(sc):
     from surfcascade_amd import synth
     from oracle import oracle as O
