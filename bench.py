@@ -355,9 +355,8 @@ def main():
         if dist is not None:  # RCCL gather: counts + capacities, then records padded to the max
             gc, gr, state["recs"] = enqueue_and_gather(det, frames, state["recs"], counts, b_max=B)
             gathered["counts"], gathered["recs"] = gc, gr
-        else:
+        else:  # stream-ordered: the next step's launches queue behind this one, no host sync per step
             det.enqueue_device(frames, state["recs"], counts)
-            det.synchronize()
 
     def check_capacity():  # N = 1: the same frames every step -> checked around the timed loop
         n = int(counts[0].item())

@@ -762,9 +762,9 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             wc.seg_shift = wc.nseg == 8 ? 0 : wc.nseg == 4 ? 1 : wc.nseg == 2 ? 2 : 3;
             wc.row_max = seg_max_for(wc.nseg);  // (<= seg_max: the LDS check above)
             if (d->opt.profile) {  // SC_OPT_PROFILE (SC_PROF_CHAIN builds): cumulative phase cycles
-                if (!d->d_prof.p) {
-                    d->d_prof.ensure(16);
-                    HIPCHK(hipMemsetAsync(d->d_prof.p, 0, 16 * sizeof(unsigned long long), d->stream));
+                if (!d->d_prof.p) {  // 16 phase totals, then per wave (start, exit) of the last launch
+                    d->d_prof.ensure(16 + 2 * 8192);
+                    HIPCHK(hipMemsetAsync(d->d_prof.p, 0, (16 + 2 * 8192) * sizeof(unsigned long long), d->stream));
                 }
                 wc.prof = d->d_prof.p;
             }
@@ -799,6 +799,26 @@ void check_chain(sc_detector *d) {
                      "deq %llu poll %llu iters %llu lanes %llu prefilter %llu thin32 %llu stages %llu "
                      "surv %llu need %llu pass %llu\n", pc[0], pc[1], pc[2], pc[3], pc[4], pc[5], pc[6],
                      pc[7], pc[8], pc[9], pc[10], pc[11], pc[12], pc[13], pc[14], pc[15]);
+        // the last launch's wave exits, as fractions of its span (first start -> last exit)
+        std::vector<unsigned long long> tw(2 * 8192);
+        HIPCHK(hipMemcpy(tw.data(), d->d_prof.p + 16, tw.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        std::vector<double> ex;
+        unsigned long long t0 = ~0ull, t1 = 0;
+        for (int i = 0; i < 8192; i++)
+            if (tw[2 * i]) {
+                t0 = std::min(t0, tw[2 * i]);
+                t1 = std::max(t1, tw[2 * i + 1]);
+            }
+        for (int i = 0; i < 8192; i++)
+            if (tw[2 * i] && t1 > t0) ex.push_back((double)(tw[2 * i + 1] - t0) / (double)(t1 - t0));
+        std::sort(ex.begin(), ex.end());
+        if (!ex.empty()) {
+            double mean = 0;
+            for (double v : ex) mean += v;
+            auto q = [&](double f) { return ex[std::min(ex.size() - 1, (size_t)(f * ex.size()))]; };
+            std::fprintf(stderr, "SC_PROF_WAVES waves %zu span %llu exit p10 %.3f p50 %.3f p90 %.3f p99 %.3f mean %.3f\n",
+                         ex.size(), t1 - t0, q(0.1), q(0.5), q(0.9), q(0.99), mean / ex.size());
+        }
     }
 }
 

@@ -802,6 +802,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     unsigned long long c_deq = 0, c_poll = 0;
     ItemStats istats;
     unsigned long long t_last = __builtin_amdgcn_s_memtime();
+    const unsigned long long t_start = t_last;
 #endif
 
     // Fused integral: the last wave of every workgroup first runs column
@@ -1186,6 +1187,13 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     if (vtot && lane_id<RM>() == 0)
         atomicAdd(&w.row_visited[(blockIdx.x * kChainWaves + wv) % (w.n_rows * a.n_frames)], vtot);
 #if SC_PROF_CHAIN
+    if (w.prof && lane_id<RM>() == 0) {  // this wave's start and exit times (launch timeline)
+        const int gw = blockIdx.x * kChainWaves + wv;
+        if (gw < 8192) {
+            w.prof[16 + 2 * gw] = t_start;
+            w.prof[17 + 2 * gw] = __builtin_amdgcn_s_memtime();
+        }
+    }
     if (w.prof && lane_id<RM>() == 0) {
         atomicAdd(&w.prof[0], c_idle);
         atomicAdd(&w.prof[1], c_setup);
