@@ -325,6 +325,7 @@ def main():
 
     def sync():
         if not stub:
+            det.synchronize()  # (also raises on a chain-kernel hand-off timeout)
             torch.cuda.synchronize()
 
     W, H, B = args.width, args.height, args.batch

@@ -15,3 +15,5 @@ for b in 1 32; do
   timeout -k 10 200 python3 bench.py --steps 3 --warmup 0 --no-cpu --latency-steps 0 --host-steps 0 --batch $b --opt profile=1 > $O/p$b.json 2> $O/p$b.err || { tail -5 $O/p$b.err; exit 1; }
   grep SC_PROF_WAVES $O/p$b.err | tail -1
 done
+unset SURFCASCADE_LIB
+bash profiles/ab.sh gpurun_out/r3g29/b1slots 2 cur s3 s3b64 -- --batch 1 --steps 50 && python3 profiles/ab_report_kernels.py gpurun_out/r3g29/b1slots > $O/b1slots.txt && cat $O/b1slots.txt
