@@ -802,7 +802,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     unsigned long long c_deq = 0, c_poll = 0;
     ItemStats istats;
     unsigned long long t_last = __builtin_amdgcn_s_memtime();
-    const unsigned long long t_start = t_last;
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();  // (chip-wide clock: per-XCD memtime counters differ)
 #endif
 
     // Fused integral: the last wave of every workgroup first runs column
@@ -901,6 +901,8 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         }
         return false;
     };
+    int spec = -1;      // this round: speculative evaluation of waiting slot `spec` (both parities)
+    unsigned spd = 0;   // bit sl: slot sl's task was evaluated speculatively
     // the chain leaves slot sl's segment at absolute position pos: hand it on
     auto finish = [&](int sl, int pos) {
         if (lane_id<RM>() == 0) {
@@ -916,10 +918,18 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             finish(sl, pos);
             return;
         }
-        for (int i = lane_id<RM>(); i < 3 * nwords; i += 64) bits0[sl * 3 * nwords + i] = 0ull;
+        if (!((spd >> sl) & 1u))  // (a speculated task's bits hold its evaluated windows)
+            for (int i = lane_id<RM>(); i < 3 * nwords; i += 64) bits0[sl * 3 * nwords + i] = 0ull;
         r[sl] = rel;
         st[sl] = 2;
     };
+#ifndef SC_SPEC_IDLE  // a wave with no active slot evaluates a waiting task's windows ahead of its entry
+#define SC_SPEC_IDLE 1
+#endif
+    static_assert(!SC_SPEC_IDLE || kSlots == 2, "speculative rounds use the two slots' descriptors");
+    // (in the 12-wave kernel, which one-frame launches use, whose tails the
+    // hand-off chains set; the 16-wave kernel would spill for it)
+    constexpr bool kSpec = SC_SPEC_IDLE && NW == 12;
 
     for (;;) {
         // 1) refill empty slots, poll the entries of waiting ones
@@ -939,6 +949,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     j0[sl] = min(nx, qq * nxs);
                     nseg[sl] = min(nx, j0[sl] + nxs) - j0[sl];
                     st[sl] = 3;  // the poll below checks the frame, then starts segment 0
+                    spd &= ~(1u << sl);
                 }
                 SC_PROF(c_deq);
             }
@@ -968,7 +979,22 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             }
             SC_PROF(c_poll);
         }
-        if (n_active == 0) {
+        spec = -1;
+        if (n_active == 0 && kSpec) {
+            // nothing to evaluate: the first waiting task not yet speculated
+            // gets both parities of its first 2*kBatch windows evaluated now,
+            // so its chain runs through them when its entry arrives (the
+            // hand-off chain's latency, not the work, sets a one-frame
+            // launch's tail)
+#pragma unroll
+            for (int sl = 0; sl < kSlots; sl++)
+                if (spec < 0 && st[sl] == 1 && !((spd >> sl) & 1u)) spec = sl;
+            if (spec >= 0) {
+                spd |= 1u << spec;
+                for (int i = lane_id<RM>(); i < 3 * nwords; i += 64) bits0[spec * 3 * nwords + i] = 0ull;
+            }
+        }
+        if (n_active == 0 && spec < 0) {
             SC_PROF(c_idle);
             if (n_wait == 0) {
                 if (drained) break;
@@ -998,20 +1024,26 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             if (v == 0x7fffffff) drained = true;
         }
 #endif
+        // descriptor sl's task: slot sl's own, or in a speculative round the
+        // waiting task `spec` at parity offset sl (selects, no dynamic index
+        // into the per-slot registers)
+#define SC_OF(v, sl) (spec < 0 ? (v)[sl] : (spec == 0 ? (v)[0] : (v)[1]))
+#define SC_ACT(sl) (spec < 0 ? st[sl] == 2 : (sl) < 2)
 #pragma unroll
         for (int sl = 0; sl < kSlots; sl++) {
             if (lane_id<RM>() == 0) {
                 SlotDesc dd{};
-                if (st[sl] == 2) {
-                    const LevelInfo &L = Lv[level[sl]];
-                    const int jb = j0[sl] + r[sl];  // the batch: jb, jb + 2, ...
-                    dd.t_off = (unsigned)((long long)frame[sl] * g.frame4 + ys[sl] * g.rowp + g.win_cell(jb));
-                    dd.nw = min(kBatch, (nseg[sl] - r[sl] + 1) >> 1);
+                if (SC_ACT(sl)) {
+                    const int lv = SC_OF(level, sl), rr = spec < 0 ? r[sl] : sl, ns_ = SC_OF(nseg, sl);
+                    const LevelInfo &L = Lv[lv];
+                    const int jb = SC_OF(j0, sl) + rr;  // the batch: jb, jb + 2, ...
+                    dd.t_off = (unsigned)((long long)SC_OF(frame, sl) * g.frame4 + SC_OF(ys, sl) * g.rowp + g.win_cell(jb));
+                    dd.nw = min(kBatch, (ns_ - rr + 1) >> 1);
                     dd.thr = L.thr;
                     dd.pre_row = L.pre_row;
                     dd.pre_col = (jb & 1) ? L.pre_col[1] : L.pre_col[0];  // (no dynamic index: scratch)
-                    dd.proj = (level[sl] * 2 + (jb & 1)) * a.K;
-                    dd.r = r[sl];
+                    dd.proj = (lv * 2 + (jb & 1)) * a.K;
+                    dd.r = rr;
                     dd.scale = L.scale;
                     dd.xb = (jb & 1) * g.step;
                     dd.cb = g.at0((unsigned)dd.xb);
@@ -1024,7 +1056,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         auto need = [&](int slot) {  // window not evaluated yet (an earlier batch may have)
             const int sl = slot / kBatch, u = slot - sl * kBatch;
             const int k = desc[sl].r + 2 * u;
-            return ((evb(sl)[k >> 6] >> (k & 63)) & 1ull) == 0ull;
+            return ((evb(spec < 0 ? sl : spec)[k >> 6] >> (k & 63)) & 1ull) == 0ull;
         };
         // the windows this round evaluates, window c*64 + lane of each slot's batch
         unsigned long long mine[kSlots][kBatchChunks];
@@ -1033,7 +1065,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
 #pragma unroll
             for (int c = 0; c < kBatchChunks; c++) {
                 const int u = c * 64 + lane_id<RM>();
-                mine[sl][c] = __ballot(st[sl] == 2 && u < desc[sl].nw && need(sl * kBatch + u));
+                mine[sl][c] = __ballot(SC_ACT(sl) && u < desc[sl].nw && need(sl * kBatch + u));
             }
         // park the slot state in LDS across the evaluation: it would otherwise
         // stay live in SGPRs / VGPR lanes through the register-heavy item loop
@@ -1043,6 +1075,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                 int *pk = park + sl * 10;
                 pk[0] = st[sl]; pk[1] = tq[sl]; pk[2] = tt[sl]; pk[3] = r[sl]; pk[4] = j0[sl];
                 pk[5] = nseg[sl]; pk[6] = frame[sl]; pk[7] = level[sl];
+                pk[8] = sl == 0 ? spec : (int)spd;
                 pk[9] = ys[sl];
             }
         }
@@ -1073,6 +1106,51 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             frame[sl] = __builtin_amdgcn_readfirstlane(pk[6]);
             level[sl] = __builtin_amdgcn_readfirstlane(pk[7]);
             ys[sl] = __builtin_amdgcn_readfirstlane(pk[9]);
+        }
+        spec = __builtin_amdgcn_readfirstlane(park[8]);
+        spd = (unsigned)__builtin_amdgcn_readfirstlane(park[10 + 8]);
+        if (kSpec && spec >= 0) {  // a speculative round: results and bits into task `spec`'s arrays, no chain step
+            const int fr = spec == 0 ? frame[0] : frame[1], y = spec == 0 ? ys[0] : ys[1], jj = spec == 0 ? j0[0] : j0[1];
+            const LevelInfo &L = Lv[spec == 0 ? level[0] : level[1]];
+            const long long gi0 = (long long)fr * w.grid_per_frame + L.grid_base +
+                                  (long long)(y / w.step) * L.nx + jj;
+            unsigned long long *ev_ = evb(spec), *gd_ = gdb(spec), *dt_ = dtb(spec);
+            float *sg = s_seg(spec);
+#pragma unroll
+            for (int d = 0; d < 2; d++)
+#pragma unroll
+                for (int c = 0; c < kBatchChunks; c++) {
+                    const unsigned long long mk = mine[d][c];
+                    if (!mk) continue;
+                    const bool in = (mk >> lane_id<RM>()) & 1ull;
+                    const int u = c * 64 + lane_id<RM>();
+                    const int k = d + 2 * u;
+                    bool good = false, det = false;
+                    if (in) {
+                        const int p = st_p[d * kBatch + u];
+                        const float sc = st_s[d * kBatch + u];
+                        if (p >= 0) {
+                            const double fin = ((double)sc + p + 1) / S;  // ObjDetector.cpp:201
+                            good = !(fin < w.stride_score);               // :214
+                        }
+                        det = p == S;
+                        sg[k] = sc;
+                        if (a.st_p) {
+                            a.st_p[gi0 + k] = (int8_t)p;
+                            a.st_s[gi0 + k] = sc;
+                        }
+                    }
+                    const unsigned long long gm = __ballot(good), dm = __ballot(det);
+                    if (lane_id<RM>() == 0) {
+                        const int base = d + 128 * c;
+                        or_spread(ev_, base, mk);
+                        if (gm) or_spread(gd_, base, gm);
+                        if (dm) or_spread(dt_, base, dm);
+                    }
+                }
+            wave_sync();
+            SC_PROF(c_merge);
+            continue;
         }
 
         // 3) per slot: merge the batch, advance the chain
@@ -1191,7 +1269,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         const int gw = blockIdx.x * kChainWaves + wv;
         if (gw < 8192) {
             w.prof[16 + 2 * gw] = t_start;
-            w.prof[17 + 2 * gw] = __builtin_amdgcn_s_memtime();
+            w.prof[17 + 2 * gw] = __builtin_amdgcn_s_memrealtime();
         }
     }
     if (w.prof && lane_id<RM>() == 0) {

@@ -306,7 +306,9 @@ def test_constant_image_no_windows(sc):
     p, s, v = det.dump_grid()
     ev = p != -2  # lazy grid: with every window rejected the chain stays on one parity
     assert (p[ev] == -1).all()
-    assert (ev == v.astype(bool)).all()
+    # every visited window was evaluated (idle waves of the 12-wave kernel may
+    # also evaluate the other parity of a waiting segment ahead of its entry)
+    assert ev[v.astype(bool)].all()
     # every row walked at stride 2*step: visited = ceil(nx/2) per row
     assert det.info("visited") == int(v.sum())
 
