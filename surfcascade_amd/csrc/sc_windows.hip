@@ -929,7 +929,10 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     static_assert(!SC_SPEC_IDLE || kSlots == 2, "speculative rounds use the two slots' descriptors");
     // (in the 12-wave kernel, which one-frame launches use, whose tails the
     // hand-off chains set; the 16-wave kernel would spill for it)
-    constexpr bool kSpec = SC_SPEC_IDLE && NW == 12;
+#ifndef SC_SPEC16
+#define SC_SPEC16 0
+#endif
+    constexpr bool kSpec = SC_SPEC_IDLE && (NW == 12 || SC_SPEC16);
 
     for (;;) {
         // 1) refill empty slots, poll the entries of waiting ones
