@@ -1267,6 +1267,8 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     // launch's words (the poll after a task's end waits for its atomics)
     if (vtot && lane_id<RM>() == 0)
         atomicAdd(&w.row_visited[(blockIdx.x * kChainWaves + wv) % (w.n_rows * a.n_frames)], vtot);
+#undef SC_OF
+#undef SC_ACT
 #if SC_PROF_CHAIN
     if (w.prof && lane_id<RM>() == 0) {  // this wave's start and exit times (launch timeline)
         const int gw = blockIdx.x * kChainWaves + wv;

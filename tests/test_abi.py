@@ -94,3 +94,12 @@ def test_frame_layouts(sc):
     assert synth.make_frames(64, 48, 2).flags["C_CONTIGUOUS"]
     with pytest.raises(ValueError):
         sc.Detector._device_frames(torch.zeros(2, 48, 64, dtype=torch.uint8))  # host tensor
+
+
+def test_option_keys_match_header():
+    """surfcascade_amd.OPTIONS names exactly the header's SC_OPT_* values."""
+    import re
+    import surfcascade_amd as sc
+    hdr = open(os.path.join(ROOT, "include", "surfcascade.h")).read()
+    defs = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"#define SC_OPT_(\w+) (\d+)", hdr)}
+    assert defs == sc.OPTIONS
