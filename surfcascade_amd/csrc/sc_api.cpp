@@ -166,6 +166,7 @@ struct sc_detector {
     DevBuf<uint8_t> d_dbg_v;    // per grid window: visited by the x chain
     int last_frames = 0;
     int last_fused = 0;  // frames of the last call integrated inside the chain kernel
+    int last_nseg = 8;   // segments per row of the last chain launch (profiling readout)
     // timing
     bool timing = false;
     struct Pending {
@@ -759,12 +760,14 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             }
             wc.frame0 = f0;
             wc.nseg = segs_for(nc);
+            d->last_nseg = wc.nseg;
             wc.seg_shift = wc.nseg == 8 ? 0 : wc.nseg == 4 ? 1 : wc.nseg == 2 ? 2 : 3;
             wc.row_max = seg_max_for(wc.nseg);  // (<= seg_max: the LDS check above)
             if (d->opt.profile) {  // SC_OPT_PROFILE (SC_PROF_CHAIN builds): cumulative phase cycles
-                if (!d->d_prof.p) {  // 16 phase totals, then per wave (start, exit) of the last launch
-                    d->d_prof.ensure(16 + 2 * 8192);
-                    HIPCHK(hipMemsetAsync(d->d_prof.p, 0, (16 + 2 * 8192) * sizeof(unsigned long long), d->stream));
+                if (!d->d_prof.p) {  // 16 phase totals, per wave (start, exit), per task (dequeue, start, finish)
+                    d->d_prof.ensure(16 + 2 * 8192 + 3 * 65536);
+                    HIPCHK(hipMemsetAsync(d->d_prof.p, 0, (16 + 2 * 8192 + 3 * 65536) * sizeof(unsigned long long),
+                                          d->stream));
                 }
                 wc.prof = d->d_prof.p;
             }
@@ -818,6 +821,32 @@ void check_chain(sc_detector *d) {
             auto q = [&](double f) { return ex[std::min(ex.size() - 1, (size_t)(f * ex.size()))]; };
             std::fprintf(stderr, "SC_PROF_WAVES waves %zu span %llu exit p10 %.3f p50 %.3f p90 %.3f p99 %.3f mean %.3f\n",
                          ex.size(), t1 - t0, q(0.1), q(0.5), q(0.9), q(0.99), mean / ex.size());
+            // task trace of the last launch, per segment: mean wait for the entry
+            // (dequeue -> start) and evaluation (start -> finish), in launch-span
+            // fractions; and the share of tasks finishing in the last 10 / 25 %
+            const int nsg = (int)d->last_nseg;
+            const size_t ntk = std::min<size_t>(65536, (size_t)d->last_frames * d->geo.rows.size() * nsg);
+            std::vector<unsigned long long> tr(3 * ntk);
+            HIPCHK(hipMemcpy(tr.data(), d->d_prof.p + 16 + 2 * 8192, tr.size() * sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost));
+            const double span = (double)(t1 - t0);
+            for (int sg = 0; sg < nsg; sg++) {
+                double wsum = 0, esum = 0, dsum = 0;
+                size_t n = 0, late10 = 0, late25 = 0;
+                for (size_t i = sg; i < ntk; i += nsg) {
+                    const unsigned long long a = tr[3 * i], b = tr[3 * i + 1], c = tr[3 * i + 2];
+                    if (!a || !b || !c || a < t0 || c < b || b < a) continue;
+                    n++;
+                    dsum += (double)(a - t0) / span;
+                    wsum += (double)(b - a) / span;
+                    esum += (double)(c - b) / span;
+                    late10 += (double)(c - t0) / span > 0.9;
+                    late25 += (double)(c - t0) / span > 0.75;
+                }
+                if (n)
+                    std::fprintf(stderr, "SC_PROF_TASKS seg %d tasks %zu dequeue %.3f wait %.4f eval %.4f finish>0.75 %zu >0.9 %zu\n",
+                                 sg, n, dsum / n, wsum / n, esum / n, late25, late10);
+            }
         }
     }
 }

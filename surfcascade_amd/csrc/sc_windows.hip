@@ -650,6 +650,9 @@ __host__ __device__ inline size_t chain_wave_bytes(int seg_max) {
 // cdna_hip_programming.md Guideline 16 (R1); the reading waves poll that
 // count and take an agent-scope acquire (chain_kernel, frame_ready).
 constexpr int kWalkRows = 8;
+#if SC_PROF_CHAIN
+constexpr long long kTraceTasks = 65536;  // task trace capacity (tasks of the last launch)
+#endif
 static_assert((kWalkRows & (kWalkRows - 1)) == 0 && kWalkRows <= 64, "walk block");
 // SC_WALK_STORE: 1 sc1 (write-through) stores; 2 plain stores + release fence
 // at the walk's end (+0.5 % kernel time); 0 none, the tables built by the
@@ -904,7 +907,17 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     int spec = -1;      // this round: speculative evaluation of waiting slot `spec` (both parities)
     unsigned spd = 0;   // bit sl: slot sl's task was evaluated speculatively
     // the chain leaves slot sl's segment at absolute position pos: hand it on
+#if SC_PROF_CHAIN  // task trace (profiling builds): realtime stamps per task at dequeue / start / finish
+    auto stamp = [&](int sl, int which) {
+        const long long ti = (long long)tt[sl] * nsg + tq[sl];
+        if (w.prof && lane_id<RM>() == 0 && ti < kTraceTasks)
+            w.prof[16 + 2 * 8192 + 3 * ti + which] = __builtin_amdgcn_s_memrealtime();
+    };
+#else
+    auto stamp = [&](int, int) {};
+#endif
     auto finish = [&](int sl, int pos) {
+        stamp(sl, 2);
         if (lane_id<RM>() == 0) {
             if (tq[sl] + 1 < nsg)
                 __hip_atomic_store(&w.entry[(long long)tt[sl] * nsg + tq[sl] + 1], pos + 1,
@@ -913,6 +926,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         st[sl] = 0;
     };
     auto start = [&](int sl, int pos) {  // the chain entered the segment at pos
+        stamp(sl, 1);
         const int rel = pos - j0[sl];
         if (rel >= nseg[sl]) {
             finish(sl, pos);
@@ -953,6 +967,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     nseg[sl] = min(nx, j0[sl] + nxs) - j0[sl];
                     st[sl] = 3;  // the poll below checks the frame, then starts segment 0
                     spd &= ~(1u << sl);
+                    stamp(sl, 0);
                 }
                 SC_PROF(c_deq);
             }
