@@ -203,9 +203,14 @@ def test_fused_integral(sc, oracle, face_cascade, n, opts):
     det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=5)).set_options(**opts)
     det.set_debug(True)
     params = oracle.Params(n_levels=5)
+    fuse, pre = opts.get("integral_fuse", 0), opts.get("integral_pre", 0) or 2
+    chunk = opts.get("chain_chunk", n)
+    launches = [min(chunk, n - f0) for f0 in range(0, n, chunk)]
+    fused = sum(nc - pre for nc in launches if fuse != 1 and nc >= (2 if fuse == 2 else 4) and nc > pre)
     for rep in range(2):
         frames = np.stack([_frame(641, 483, 3000 + 37 * rep + k) for k in range(n)])
         batch = det.detect_batch(frames)
+        assert det.info("fused_frames") == fused
         layout, _ = oracle.grid_layout(641, 483, params)
         for k in range(n):
             T = oracle.integral(frames[k])
