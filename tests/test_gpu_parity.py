@@ -190,7 +190,7 @@ def test_integral_batch_frames(sc, oracle, n):
         assert T.view(np.uint32).tobytes() == oracle.integral(frames[k]).view(np.uint32).tobytes()
 
 
-@pytest.mark.parametrize("n,opts", [(2, {"integral_fuse": 2}), (5, {"integral_pre": 2}),
+@pytest.mark.parametrize("n,opts", [(2, {"integral_fuse": 2, "integral_pre": 1}), (5, {"integral_pre": 2}),
                                     (7, {"chain_chunk": 3, "integral_fuse": 2}), (4, {}),
                                     (4, {"integral_fuse": 1}), (6, {"integral_pre": 1, "chain_waves": 12})])
 def test_fused_integral(sc, oracle, face_cascade, n, opts):
