@@ -816,7 +816,10 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
 #define SC_WALKERS 1
 #endif
     if (w.int_walks > 0 && wv >= kChainWaves - SC_WALKERS) {
-        __builtin_amdgcn_s_setprio(2);  // latency-bound: issue ahead of the gathers
+#ifndef SC_WALK_PRIO
+#define SC_WALK_PRIO 2
+#endif
+        __builtin_amdgcn_s_setprio(SC_WALK_PRIO);  // latency-bound: issue ahead of the gathers
         for (;;) {
             int t = 0;
             if (lane_id<RM>() == 0) t = atomicAdd(&w.int_ctl[0], 1);
