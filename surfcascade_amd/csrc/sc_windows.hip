@@ -944,8 +944,9 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
 #define SC_SPEC_IDLE 1
 #endif
     static_assert(!SC_SPEC_IDLE || kSlots == 2, "speculative rounds use the two slots' descriptors");
-    // (in the 12-wave kernel, which one-frame launches use, whose tails the
-    // hand-off chains set; the 16-wave kernel would spill for it)
+    // (one-frame launches, in the 12-wave kernel they use: their tails are
+    // the hand-off chains' latency; a bandwidth-bound launch pays for the
+    // extra windows -- C4 +3.9 % -- and the 16-wave kernel would spill)
 #ifndef SC_SPEC16
 #define SC_SPEC16 0
 #endif
@@ -1001,7 +1002,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             SC_PROF(c_poll);
         }
         spec = -1;
-        if (n_active == 0 && kSpec) {
+        if (n_active == 0 && kSpec && a.n_frames == 1) {  // (one-frame launches: latency-bound)
             // nothing to evaluate: the first waiting task not yet speculated
             // gets both parities of its first 2*kBatch windows evaluated now,
             // so its chain runs through them when its entry arrives (the
