@@ -645,9 +645,15 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
         ra.zero[3] = d->d_entry.p;
         ra.zero_n[3] = entry_words(std::min(chunk, n));
     }
+    // the frames whose column pass is two-pass (the first launch's `pre`
+    // frames when fused, else all of a 1-3-frame call): rowcarry4 writes
+    // their R rows too, so rowfull does not run for them
+    const bool two_pass_all = d->opt.integral_passes ? d->opt.integral_passes == 2 : n <= 3;
+    const bool two_pass_pre = d->opt.integral_passes ? d->opt.integral_passes == 2 : pre <= 3;
+    ra.rfull_n = fuse ? (two_pass_pre ? std::min(pre, n) : 0) : (two_pass_all ? n : 0);
     hipEvent_t e0 = nullptr;
     timed_begin(d, &e0);
-    sc::launch_rowscan(ra, n, d->stream);
+    const bool have_r = sc::launch_rowscan(ra, n, d->stream);
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_ROWSCAN, e0);
 
@@ -660,17 +666,15 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
 #else
     if (fuse) {  // only the first `pre` frames of each launch here
 #endif
-        const bool two_pass = d->opt.integral_passes ? d->opt.integral_passes == 2 : pre <= 3;
         for (int f0 = 0; f0 < n; f0 += chunk) {
             sc::RowScanArgs rc = ra;
             rc.frames = d_frames + (long long)f0 * H * stride;
             rc.table = d->d_table.p + (size_t)f0 * g.tg.frame4;
             rc.carry = d->d_carry.p + f0 * carry_frame;
-            sc::launch_colscan(rc, std::min(pre, n - f0), two_pass, d->stream);
+            sc::launch_colscan(rc, std::min(pre, n - f0), two_pass_pre, d->stream, have_r && f0 == 0);
         }
     } else {
-        const bool two_pass = d->opt.integral_passes ? d->opt.integral_passes == 2 : n <= 3;
-        sc::launch_colscan(ra, n, two_pass, d->stream);
+        sc::launch_colscan(ra, n, two_pass_all, d->stream, have_r);
     }
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_COLSCAN, e0);

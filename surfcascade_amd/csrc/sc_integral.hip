@@ -149,6 +149,9 @@ __global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
     // x = 0 clamps to itself
     uint32_t lu = u0 & 0xffu, lc = c0 & 0xffu, ld = d0 & 0xffu;
     uint32_t run[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    // frames whose column pass is colsum (two-pass): their R rows are written
+    // here, so rowfull_kernel does not run for them
+    const bool write_r = frame < a.rfull_n;
     for (int p = 0; p < np; p++) {
         uint32_t u1, c1, d1;
         load(p + 1, u1, c1, d1);
@@ -165,6 +168,7 @@ __global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
         const unsigned long long U = window(u0, lu, nu), C = window(c0, lc, nc), D = window(d0, ld, nd);
         const int x0 = p * 256 + 4 * lane;
         uint32_t G[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+        uint32_t Pc[4][8];  // the lane's inclusive prefix through column j (R rows: rowfull's cells)
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int x = x0 + j;
@@ -176,6 +180,8 @@ __global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
                 G[0] += sat_sub(a0, b0); G[1] += sat_sub(b0, a0); G[2] += sat_sub(c0_, d0_); G[3] += sat_sub(d0_, c0_);
                 G[4] += sat_sub(a1, b1); G[5] += sat_sub(b1, a1); G[6] += sat_sub(c1_, d1_); G[7] += sat_sub(d1_, c1_);
             }
+#pragma unroll
+            for (int ch = 0; ch < 8; ch++) Pc[j][ch] = G[ch];
         }
         // 16-bit channel pairs: a pass's prefix stays < 64 x 4 x 255 < 2^16
         uint32_t q[4] = {G[0] | (G[1] << 16), G[2] | (G[3] << 16), G[4] | (G[5] << 16), G[6] | (G[7] << 16)};
@@ -185,6 +191,22 @@ __global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
             const uint32_t incl = wave_scan(q[k]);
             e[k] = incl - q[k];  // exclusive: the columns of the pass left of this lane
             q[k] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);  // the pass's totals
+        }
+        if (write_r) {  // R_y[x+1] = the exact row prefix through column x, into table row y+1
+            float4 *trow = tab + (long long)(y + 1) * g.rowp;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int x = x0 + j;
+                if (x < W) {
+                    uint4 r0, r1;
+                    r0.x = run[0] + (e[0] & 0xffffu) + Pc[j][0]; r0.y = run[1] + (e[0] >> 16) + Pc[j][1];
+                    r0.z = run[2] + (e[1] & 0xffffu) + Pc[j][2]; r0.w = run[3] + (e[1] >> 16) + Pc[j][3];
+                    r1.x = run[4] + (e[2] & 0xffffu) + Pc[j][4]; r1.y = run[5] + (e[2] >> 16) + Pc[j][5];
+                    r1.z = run[6] + (e[3] & 0xffffu) + Pc[j][6]; r1.w = run[7] + (e[3] >> 16) + Pc[j][7];
+                    reinterpret_cast<uint4 *>(trow)[g.at(x + 1, 0)] = r0;
+                    reinterpret_cast<uint4 *>(trow)[g.at(x + 1, 1)] = r1;
+                }
+            }
         }
         const int s = p * 8 + (lane >> 3);  // 32-column strip starting at this lane (lane % 8 == 0)
         if ((lane & 7) == 0 && s < ns) {
@@ -387,18 +409,23 @@ __global__ __launch_bounds__(64) void colsum4_kernel(RowScanArgs a) {
 #ifndef SC_RC_DWORD  // rowcarry4 (dword loads) when the rows start 4-B aligned
 #define SC_RC_DWORD 1
 #endif
-void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
+bool launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
     const bool aligned = ((uintptr_t)a.frames & 3u) == 0 && (a.stride & 3) == 0;
-    if (SC_RC_DWORD && aligned)
+    if (SC_RC_DWORD && aligned) {
         hipLaunchKernelGGL(rowcarry4_kernel, dim3(a.g.H, n_frames), dim3(64), 0, s, a);
-    else
-        hipLaunchKernelGGL(rowcarry_kernel, dim3((a.g.H + kRcRows - 1) / kRcRows, n_frames), dim3(64 * kRcRows), 0, s, a);
+        return a.rfull_n > 0;
+    }
+    RowScanArgs b = a;
+    b.rfull_n = 0;
+    hipLaunchKernelGGL(rowcarry_kernel, dim3((a.g.H + kRcRows - 1) / kRcRows, n_frames), dim3(64 * kRcRows), 0, s, b);
+    return false;
 }
 
-void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s) {
+void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s, bool have_r) {
     const int ns64 = (a.g.W + 2 * kStrip - 1) / (2 * kStrip);
     if (two_pass) {
-        hipLaunchKernelGGL(rowfull_kernel, dim3(ns64 * 2, a.g.H, n_frames), dim3(64), 0, s, a);
+        if (!have_r)  // (rowcarry4 wrote the R rows already)
+            hipLaunchKernelGGL(rowfull_kernel, dim3(ns64 * 2, a.g.H, n_frames), dim3(64), 0, s, a);
         if (SC_COLSUM4)
             hipLaunchKernelGGL(colsum4_kernel, dim3(ns64 * 8, n_frames), dim3(64), 0, s, a);
         else

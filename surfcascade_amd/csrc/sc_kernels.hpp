@@ -113,6 +113,8 @@ struct RowScanArgs {
     // dispatch each
     int *zero[4];
     long long zero_n[4];
+    int rfull_n;  // rowcarry4: frames [0, rfull_n) also get their exact row prefixes R written
+                  // into the table (the two-pass column pass's input; rowfull then skipped)
 };
 
 // Cascade kernel: persistent workgroups of 4 independent waves; a task is
@@ -235,10 +237,11 @@ void launch_mine_scan(const MineArgs &a, hipStream_t s);
 void launch_mine_scatter(const MineArgs &a, hipStream_t s);
 void launch_features(const FeatureArgs &a, hipStream_t s);
 
-// integral pass 1 (rowcarry) and pass 2 (colstrip), sc_integral.hip
-void launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s);
-// two_pass: rowfull + colsum (small batches), else colstrip
-void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s);
+// integral pass 1 (rowcarry4 / rowcarry), sc_integral.hip; returns whether
+// the R rows of frames [0, a.rfull_n) were written (rowcarry4)
+bool launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s);
+// two_pass: rowfull + colsum (small batches; rowfull skipped when have_r), else colstrip
+void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s, bool have_r = false);
 // Per-detector launch configuration: the device's CU count (queried once
 // per detector, no process-wide cache) and the SC_OPT_* launch options.
 struct LaunchCfg {
