@@ -372,7 +372,10 @@ __global__ __launch_bounds__(64) void colsum_kernel(RowScanArgs a) {
 // 16 columns x 4 channels, one dword per row and lane, so a lane keeps 4x
 // the rows of loads in flight in the same registers (the walk is bound by
 // the load latency: 120 walks for a 1080p frame, one per SIMD at most).
-constexpr int kSumAhead4 = 48;
+#ifndef SC_SUM_AHEAD4
+#define SC_SUM_AHEAD4 48
+#endif
+constexpr int kSumAhead4 = SC_SUM_AHEAD4;
 __global__ __launch_bounds__(64) void colsum4_kernel(RowScanArgs a) {
     const int nb = gridDim.x * gridDim.y, b = blockIdx.x + blockIdx.y * gridDim.x;
     const int xq = b % kXcds, q = nb / kXcds, r = nb % kXcds;
