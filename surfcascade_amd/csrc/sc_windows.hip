@@ -800,6 +800,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     int u = (int)((blockIdx.x / kXcds * kChainWaves + wv) % kSubQ);
     bool drained = false;
     unsigned idle = 0;  // rounds with every task waiting for its entry
+    unsigned long long idle_t0 = 0;  // when the current wait began (s_memrealtime)
 #if SC_PROF_CHAIN
     unsigned long long c_idle = 0, c_setup = 0, c_eval = 0, c_merge = 0, n_rounds = 0, n_slots = 0;
     unsigned long long c_deq = 0, c_poll = 0;
@@ -1023,14 +1024,23 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                 continue;
             }
             __builtin_amdgcn_s_sleep(4);
-            if (++idle == (1u << 24)) {  // a lost hand-off must not hang the GPU
+            // a lost hand-off must not hang the GPU: after 0.5 s of waiting (the
+            // chip-wide 100 MHz clock), or once any wave's watchdog has fired,
+            // the waiting tasks start anyway and the error word says so
+            if (idle++ == 0) idle_t0 = __builtin_amdgcn_s_memrealtime();
+            if ((idle & 255u) == 0u) {
+                int e = 0;
+                if (lane_id<RM>() == 0) e = __hip_atomic_load(w.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__builtin_amdgcn_readfirstlane(e) != 0 ||
+                    __builtin_amdgcn_s_memrealtime() - idle_t0 > 50000000ull) {
 #pragma unroll
-                for (int sl = 0; sl < kSlots; sl++)
-                    if (st[sl] == 1 || st[sl] == 3) {
-                        if (lane_id<RM>() == 0) atomicAdd(w.err, 1);
-                        start(sl, j0[sl]);
-                    }
-                idle = 0;
+                    for (int sl = 0; sl < kSlots; sl++)
+                        if (st[sl] == 1 || st[sl] == 3) {
+                            if (lane_id<RM>() == 0) atomicAdd(w.err, 1);
+                            start(sl, j0[sl]);
+                        }
+                    idle = 0;
+                }
             }
             continue;
         }
