@@ -407,6 +407,45 @@ __global__ __launch_bounds__(64) void colsum4_kernel(RowScanArgs a) {
     }
 }
 
+// colsum in table order: a wave owns 64 consecutive floats of every table row
+// (8 cells x 8 channels when the 8 channels sit together, 16 cells x 4
+// otherwise), lane = (cell, channel), so each row's load and store is two
+// whole 128-B lines instead of colsum4's 16 columns spread over the `ph`
+// phase planes.  Cells of the plane padding (and column 0) are skipped; the
+// per-element f32 step and its order are colsum4's.
+#ifndef SC_COLSUM_PLANE
+#define SC_COLSUM_PLANE 1
+#endif
+__global__ __launch_bounds__(64) void colsum_plane_kernel(RowScanArgs a) {
+    const TableGeom g = a.g;
+    const int frame = blockIdx.y, lane = threadIdx.x;
+    const int fi = blockIdx.x * 64 + lane;  // float within a table row
+    const int f4 = fi >> 2, plane_cells = g.ph * g.Qp;
+    const int ci = g.cs == 2 ? f4 >> 1 : f4 % plane_cells;  // cell index within its half
+    const int col = (ci % g.Qp) * g.ph + ci / g.Qp;         // table column (x + 1)
+    if (col < 1 || col > g.W) return;  // (no cross-lane work in this pass)
+    float *cellp = reinterpret_cast<float *>(a.table + (long long)frame * g.frame4 + g.rowp) + fi;  // table row 1
+    const uint32_t *rp = reinterpret_cast<const uint32_t *>(cellp);
+    const long long rs = (long long)g.rowp * 4;  // floats per table row
+    const int H = g.H;
+    float S = 0.0f;
+    uint32_t ra[kSumAhead4];
+#pragma unroll
+    for (int k = 0; k < kSumAhead4; k++) ra[k] = rp[min(k, H - 1) * rs];
+    for (int y0 = 0; y0 < H; y0 += kSumAhead4) {
+        uint32_t rb[kSumAhead4];
+#pragma unroll
+        for (int k = 0; k < kSumAhead4; k++) rb[k] = rp[min(y0 + kSumAhead4 + k, H - 1) * rs];
+#pragma unroll
+        for (int k = 0; k < kSumAhead4; k++) {
+            S = S + (float)ra[k];  // the f32 column step, colstrip's order
+            if (y0 + k < H) cellp[(y0 + k) * rs] = S;
+        }
+#pragma unroll
+        for (int k = 0; k < kSumAhead4; k++) ra[k] = rb[k];
+    }
+}
+
 }  // namespace
 
 #ifndef SC_RC_DWORD  // rowcarry4 (dword loads) when the rows start 4-B aligned
@@ -429,7 +468,12 @@ void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream
     if (two_pass) {
         if (!have_r)  // (rowcarry4 wrote the R rows already)
             hipLaunchKernelGGL(rowfull_kernel, dim3(ns64 * 2, a.g.H, n_frames), dim3(64), 0, s, a);
-        if (SC_COLSUM4)
+        // table order from 2 frames (C2's two prebuilt frames: 0.087 -> 0.062
+        // ms); one frame stays with colsum4 (0.054 vs 0.059 ms: its 240 walks
+        // are latency-bound, profiles/r3/g51)
+        if (SC_COLSUM_PLANE && n_frames >= 2)
+            hipLaunchKernelGGL(colsum_plane_kernel, dim3(a.g.rowp / 16, n_frames), dim3(64), 0, s, a);
+        else if (SC_COLSUM4)
             hipLaunchKernelGGL(colsum4_kernel, dim3(ns64 * 8, n_frames), dim3(64), 0, s, a);
         else
             hipLaunchKernelGGL(colsum_kernel, dim3(ns64 * 2, n_frames), dim3(64), 0, s, a);
