@@ -299,7 +299,7 @@ def main():
     import torch
     import surfcascade_amd as sc
     from surfcascade_amd import synth
-    from surfcascade_amd.dist import enqueue_and_gather, merge_records, shard_range
+    from surfcascade_amd.dist import StreamGather, enqueue_and_gather, merge_records, shard_range
 
     stub = args.stub
     if stub:
@@ -370,6 +370,16 @@ def main():
         step()
     if dist is None:
         check_capacity()
+    # N > 1, timed steps: counts and records in one buffer, one all_gather per
+    # step on the stream, no host round trip (dist.StreamGather); the warm-up
+    # above sized the buffers (every rank alike), one more warm step runs
+    # through it, and its overflow check runs after the timed loop
+    sg = None
+    if dist is not None:
+        sg = StreamGather(B, state["recs"].numel() // sc.RECORD_DTYPE.itemsize, dev)
+        sg.step(det, frames)
+        sync()
+        sg.result()
     grid = det.info("grid_windows")
     det.get_timing()  # discard
     det.set_timing(True)
@@ -378,7 +388,10 @@ def main():
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        if sg is not None:
+            sg.step(det, frames)
+        else:
+            step()
     sync()
     if dist is not None:
         dist.barrier()
@@ -389,6 +402,8 @@ def main():
     fused_frames = det.info("fused_frames")  # (before the latency / host legs replace the last call)
     if dist is None:
         check_capacity()
+    else:  # the last timed step's gather (raises if any rank's buffer overflowed)
+        gathered["counts"], gathered["recs"] = sg.result()
     # single-frame latency (C2 names "1080p frame"): batch-1 steps, device-resident
     lat = None
     if args.latency_steps > 0 and not grid_shard and not stub:

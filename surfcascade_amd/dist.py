@@ -139,6 +139,56 @@ def enqueue_and_gather(det, frames, recs, counts, group=None, b_max=None):
     return gc, gr, recs
 
 
+class StreamGather:
+    """The gather for a steady stream of equal steps, with no host round trip
+    per step.  A rank's counts and records share one device buffer
+    (`recs` | `counts`, a fixed size agreed by every rank at construction),
+    sc_enqueue_device writes both, and one all_gather of the whole buffer
+    follows on the current stream (RCCL orders it after the scan, the next
+    scan after it).  The step never reads a count on the host, so the GPU runs
+    scan, gather, scan, ... back to back; `result()` syncs once, then raises
+    RecordOverflow for a rank whose count exceeded the capacity (its buffer
+    lost records: re-run that step with `enqueue_and_gather`, which grows the
+    buffers).  `enqueue_and_gather` remains the checked per-step form.
+    b: frames per rank (the same on every rank); capacity: records."""
+
+    def __init__(self, b, capacity, device, group=None):
+        import torch
+        import torch.distributed as dist
+        self.group, self.b, self.capacity = group, int(b), int(capacity)
+        self.world = dist.get_world_size(group)
+        self.cap_bytes = self.capacity * RECORD_DTYPE.itemsize
+        n = self.cap_bytes + 4 * (1 + self.b)
+        self.buf = torch.zeros(n, dtype=torch.uint8, device=device)
+        self.recs = self.buf[: self.cap_bytes]
+        self.counts = self.buf[self.cap_bytes:].view(torch.int32)
+        self.out = torch.zeros(self.world, n, dtype=torch.uint8, device=device)
+        mine = torch.tensor([self.b, self.capacity], dtype=torch.int64, device=device)
+        got = [torch.zeros_like(mine) for _ in range(self.world)]
+        dist.all_gather(got, mine, group=group)
+        for r, g in enumerate(got):
+            if g.tolist() != [self.b, self.capacity]:
+                raise ValueError("StreamGather needs one layout on every rank: rank %d has (frames, capacity) %s, "
+                                 "this rank (%d, %d)" % (r, g.tolist(), self.b, self.capacity))
+
+    def step(self, det, frames):
+        import torch.distributed as dist
+        det.enqueue_device(frames, self.recs, self.counts)
+        dist.all_gather(list(self.out.unbind(0)), self.buf, group=self.group)
+
+    def result(self):
+        """(per-rank counts [1+b] int32, per-rank record bytes) of the last step."""
+        host = self.out.cpu().numpy()
+        gc, gr = [], []
+        for r in range(self.world):
+            c = host[r, self.cap_bytes:].view(np.int32).copy()
+            if int(c[0]) > self.capacity:
+                raise RecordOverflow(r, int(c[0]), self.capacity)
+            gc.append(c)
+            gr.append(host[r, : self.cap_bytes].copy())
+        return gc, gr
+
+
 def merge_records(gathered_counts, gathered_recs, frame_offsets):
     """Decode every rank's records, shift frames to global indices, sort.
     A rank whose count exceeds the records it sent raises RecordOverflow."""

@@ -1,7 +1,8 @@
 """The RCCL gather on a real GPU: one rank, backend "nccl"
 (RCCL), the same code path bench.py takes at N > 1 -- counts + capacities
 all_gather, the grow-and-rescan on overflow, the padded record all_gather --
-against sc_detect_batch of the same frames.  The multi-rank logic is covered
+against sc_detect_batch of the same frames, and the stream-ordered
+StreamGather of bench.py's timed steps.  The multi-rank logic is covered
 by the gloo tests (tests/test_dist.py); N > 1 on GPUs runs in the driver's
 scaling bench.  Runs in a child process so the process group is torn down
 with it."""
@@ -25,7 +26,7 @@ import torch.distributed as dist
 import surfcascade_amd as sc
 from oracle import oracle as O
 from surfcascade_amd import synth
-from surfcascade_amd.dist import enqueue_and_gather, merge_records
+from surfcascade_amd.dist import StreamGather, enqueue_and_gather, merge_records
 
 torch.cuda.set_device(0)
 dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
@@ -48,6 +49,23 @@ exp = sorted((f,) + (int(r["level"]), int(r["y"]), int(r["x"]), float(r["score"]
 assert got == exp and len(got) > 100, (len(got), len(exp))
 gc2, gr2, _ = enqueue_and_gather(det, dev, recs2, counts)  # second step: no regrowth
 assert [list(c) for c in gc2] == [list(c) for c in gc]
+# bench.py's timed steps: counts + records in one buffer, one all_gather per
+# step on the stream, no host sync per step (dist.StreamGather)
+sg = StreamGather(len(frames), recs2.numel() // sc.RECORD_DTYPE.itemsize, "cuda:0")
+for _ in range(3):
+    sg.step(det, dev)
+det.synchronize()
+torch.cuda.synchronize()
+gc3, gr3 = sg.result()
+assert sorted(key(r) for r in merge_records(gc3, gr3, [0])) == exp
+sg_small = StreamGather(len(frames), 8, "cuda:0")  # overflow: raised, never truncated
+sg_small.step(det, dev)
+torch.cuda.synchronize()
+try:
+    sg_small.result()
+    raise AssertionError("StreamGather overflow not raised")
+except sc.dist.RecordOverflow:
+    pass
 dist.barrier()
 dist.destroy_process_group()
 print("ok", len(got))
