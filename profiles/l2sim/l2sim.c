@@ -116,10 +116,13 @@ static void item_cells(const Geom *g, const int32_t *rect, float scale, int y, i
  * task of either class (the class of a task = grp_of_level of its level, 1 =
  * big), the other slots only class-0 tasks (concurrency limit for the wide
  * levels); big_slots < 0: one queue. */
+static int g_cell_bytes = 16; /* 12: u24-packed half cells (lossless for values < 2^24) */
+void l2sim_set_cell_bytes(int b) { g_cell_bytes = b; }
 int l2sim_run(const Geom *g, int n_tasks, const int64_t *it_off, const int32_t *items,
               const int32_t *rects, const float *scale, int conc, int cus, int l1_lines,
               int l2_lines, const int32_t *xcd_of_task, const int32_t *grp_of_level, int n_groups,
-              int64_t *stats, int big_slots) {
+              int64_t *stats, int big_slots, const int32_t *grp_of_weak, const int32_t *alt_of_weak,
+              const Geom *g2, int64_t alt_base) {
     memset(stats, 0, sizeof(int64_t) * 4 * n_groups);
     for (int x = 0; x < 8; x++) {
         /* this XCD's tasks in queue order */
@@ -156,7 +159,7 @@ int l2sim_run(const Geom *g, int n_tasks, const int64_t *it_off, const int32_t *
             live += act[s] >= 0;
         }
         int64_t cells[64][20];
-        uint64_t lines[64];
+        uint64_t lines[128];
         while (live > 0) {
             for (int s = 0; s < conc; s++) {
                 int t = act[s];
@@ -167,14 +170,20 @@ int l2sim_run(const Geom *g, int n_tasks, const int64_t *it_off, const int32_t *
                 int grp = 0;
                 for (int i = 0; i < n; i++) {
                     const int32_t *it = items + 4 * (pos[s] + i);
-                    grp = grp_of_level[it[0]];
-                    item_cells(g, rects + 4 * it[3], scale[it[0]], it[1], g->step * it[2], cells[i]);
+                    grp = grp_of_weak ? grp_of_weak[it[3]] : grp_of_level[it[0]];
+                    if (alt_of_weak && alt_of_weak[it[3]]) {
+                        item_cells(g2, rects + 4 * it[3], scale[it[0]], it[1], g->step * it[2], cells[i]);
+                        for (int m = 0; m < 20; m++) cells[i][m] += alt_base;
+                    } else {
+                        item_cells(g, rects + 4 * it[3], scale[it[0]], it[1], g->step * it[2], cells[i]);
+                    }
                 }
                 /* 20 wave-level loads; distinct lines per load = L1 accesses */
                 for (int m = 0; m < 20; m++) {
                     int nl = 0;
-                    for (int i = 0; i < n; i++) {
-                        const uint64_t ln = (uint64_t)(cells[i][m] * 16) >> 7;
+                    for (int i = 0; i < 2 * n; i++) {
+                        const uint64_t b0 = (uint64_t)(cells[i >> 1][m] * g_cell_bytes);
+                        const uint64_t ln = (i & 1) ? (b0 + g_cell_bytes - 1) >> 7 : b0 >> 7;
                         int seen = 0;
                         for (int u = 0; u < nl; u++)
                             if (lines[u] == ln) {

@@ -32,7 +32,8 @@ def lib():
         subprocess.check_call(["gcc", "-O2", "-shared", "-fPIC", "-o", so, src])
     L = ctypes.CDLL(so)
     L.l2sim_run.argtypes = [ctypes.POINTER(Geom), ctypes.c_int] + [ctypes.c_void_p] * 4 + \
-        [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int] + \
+        [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64]
     return L
 
 
@@ -119,6 +120,11 @@ def main():
     ap.add_argument("--big-split", help="big levels: SEGS:ROWCLASSES (e.g. 4:2)")
     ap.add_argument("--big-from", type=int, default=13)
     ap.add_argument("--xcd-split", type=int, help="small levels on this many XCDs, big on the rest")
+    ap.add_argument("--cell-bytes", type=int, default=16, help="bytes per half cell (12: u24 packing)")
+    ap.add_argument("--group", default="level", choices=("level", "stage"))
+    ap.add_argument("--alt-from", type=int, default=-1,
+                    help="stages >= this read a second table copy in --alt-layout (hybrid layouts)")
+    ap.add_argument("--alt-layout", default="inter", choices=("split", "inter", "pix"))
     ap.add_argument("--big-slots", type=int, default=-1,
                     help="two queues: only this many of the conc slots take big-level tasks")
     a = ap.parse_args()
@@ -143,16 +149,35 @@ def main():
     scale = np.array([np.float32(O.level_len(70, i)) / np.float32(40) for i in range(24)], np.float32)
     grp = np.array([0 if i < a.big_from else 1 for i in range(24)], np.int32)
     g = geometry(1920, 1080, 3, a.layout)
-    stats = np.zeros((2, 4), np.int64)
+    off = np.concatenate([[0], np.cumsum(casc.n_weak)])
+    stage_of = np.zeros(len(rects), np.int32)
+    for st in range(casc.n_stages):
+        stage_of[off[st]:off[st + 1]] = st
+    if a.group == "stage":
+        gw, names = stage_of, ["stage %d" % st for st in range(casc.n_stages)]
+    else:
+        gw, names = None, ["levels 0-12", "levels 13-23"]
+    ng = len(names)
+    alt = (stage_of >= a.alt_from).astype(np.int32) if a.alt_from >= 0 else None
+    if a.alt_layout == "pix":  # one plane, 32-B pixels: cell(y, x, h) = y*rowp + 2x + h
+        Q = 1921
+        g2 = Geom(1920, 1080, 3, 1, Q, 2 * Q, 1, 2)
+    else:
+        g2 = geometry(1920, 1080, 3, a.alt_layout)
+    alt_base = 1082 * g.rowp + 4096
+    stats = np.zeros((ng, 4), np.int64)
     L = lib()
+    L.l2sim_set_cell_bytes(a.cell_bytes)
     L.l2sim_run(ctypes.byref(g), len(it_off) - 1, it_off.ctypes.data, items.ctypes.data, rec.ctypes.data,
-                scale.ctypes.data, a.conc, 32, 256, int(a.l2_mib * 8192), xcd.ctypes.data, grp.ctypes.data, 2,
-                stats.ctypes.data, a.big_slots)
+                scale.ctypes.data, a.conc, 32, 256, int(a.l2_mib * 8192), xcd.ctypes.data, grp.ctypes.data, ng,
+                stats.ctypes.data, a.big_slots, gw.ctypes.data if gw is not None else None,
+                alt.ctypes.data if alt is not None else None, ctypes.byref(g2), alt_base)
     out = {"args": vars(a), "items": int(len(items)), "build_s": t1 - t0, "sim_s": time.time() - t1}
-    for gi, name in enumerate(("levels 0-12", "levels 13-23")):
+    for gi, name in enumerate(names):
         acc, m1, h2, m2 = (int(v) for v in stats[gi])
         if acc:
-            out[name] = {"l1_accesses": acc, "l1_miss": m1 / acc, "l2_hit": h2 / max(m1, 1), "l2_misses": m2}
+            out[name] = {"l1_accesses": acc, "l1_miss": round(m1 / acc, 4), "l2_hit": round(h2 / max(m1, 1), 4),
+                         "l2_misses": m2}
     tot = stats.sum(0)
     out["all"] = {"l1_accesses": int(tot[0]), "l1_miss": tot[1] / tot[0], "l2_hit": tot[2] / max(tot[1], 1),
                   "l2_misses": int(tot[3])}
