@@ -234,10 +234,6 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
                               /* launch has 2+ frames                          */
 #define SC_OPT_INTEGRAL_PRE 19 /* fused: frames per launch integrated before   */
                               /* the chain kernel (0: default 2)               */
-#define SC_OPT_TABLE_U24 20   /* chain-kernel gathers from a packed copy of    */
-                              /* the table (12-B half-cells, values < 2^24     */
-                              /* exactly; f32 fallback above): 0 auto, 1 off,  */
-                              /* 2 on                                          */
 int sc_detector_set_option(sc_detector *d, int option, int64_t value);
 
 /* Enable per-window debug records (grid order) for the next detect calls. */

@@ -130,7 +130,6 @@ struct sc_detector {
         int chain_waves = 0;             // chain kernel waves per workgroup (0 auto)
         int integral_fuse = 0;           // column walks inside the chain kernel: 0 auto, 1 never, 2 from 2 frames
         int integral_pre = 0;            // fused: frames integrated before the chain kernel (0: 2)
-        int table_u24 = 0;               // chain gathers from the packed table copy: 0 auto, 1 off, 2 on
     } opt;
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
@@ -151,7 +150,6 @@ struct sc_detector {
     DevBuf<uint8_t> d_frames;
     PinnedBuf h_stage;           // host frames -> pinned -> d_frames (upload_frames)
     DevBuf<float4> d_table;
-    DevBuf<unsigned> d_table24;  // the packed copy (3 dwords per float4 cell), chain kernel only
     DevBuf<uint32_t> d_carry;    // integral pass 1 -> pass 2: per-strip row prefixes
     int table_frames = 0;
     DevBuf<sc_det_record> d_out;
@@ -193,7 +191,7 @@ struct sc_detector {
         d_levels.release(); d_rows.release(); d_proj.release(); d_tasks.release();
         d_proj_all.release(); d_mine_cnt.release(); d_mine_off.release(); d_mine_win.release();
         d_feat.release();
-        d_frames.release(); d_table.release(); d_table24.release(); d_carry.release(); d_out.release(); d_counters.release();
+        d_frames.release(); d_table.release(); d_carry.release(); d_out.release(); d_counters.release();
         d_visited.release(); d_queues.release(); d_entry.release(); d_st_p.release(); d_st_s.release();
         d_dbg_v.release(); d_prof.release();
         h_stage.release();
@@ -627,10 +625,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     // vs 25.88 ms per 8-frame step, profiles/r3/g21).
     const int pre = d->opt.integral_pre > 0 ? d->opt.integral_pre : 2;
     const int fuse_from = d->opt.integral_fuse == 2 ? 2 : 4;
-    // Packed table (SC_OPT_TABLE_U24): the chain kernel's item gathers read
-    // 12-B half-cells instead of 16
-    const bool u24 = chain && d->opt.table_u24 == 2;
-    const bool fuse = chain && !u24 && d->opt.integral_fuse != 1 && std::min(chunk, n) >= fuse_from &&
+    const bool fuse = chain && d->opt.integral_fuse != 1 && std::min(chunk, n) >= fuse_from &&
                       std::min(chunk, n) > pre &&
                       (d->opt.integral_fuse == 2 || g.tg.frame4 * 16 <= (128ll << 20));
 
@@ -680,10 +675,6 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
         }
     } else {
         sc::launch_colscan(ra, n, two_pass_all, d->stream, have_r);
-    }
-    if (u24) {
-        d->d_table24.ensure((size_t)g.tg.frame4 * n * 3);
-        sc::launch_pack24(d->d_table.p, d->d_table24.p, (long long)g.tg.frame4 * n, d->stream);
     }
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_COLSCAN, e0);
@@ -752,7 +743,6 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             sc::CascadeArgs cc = ca;
             sc::WalkArgs wc = wk;
             cc.table = d->d_table.p + (size_t)f0 * g.tg.frame4;
-            cc.table24 = u24 ? reinterpret_cast<const char *>(d->d_table24.p + (size_t)f0 * g.tg.frame4 * 3) : nullptr;
             cc.n_frames = nc;
             cc.st_p = d->debug ? d->d_st_p.p + (size_t)f0 * g.grid : nullptr;
             cc.st_s = d->debug ? d->d_st_s.p + (size_t)f0 * g.grid : nullptr;
@@ -1493,7 +1483,6 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
             case SC_OPT_INTEGRAL_PASSES: o.integral_passes = range(0, 2); regeo = false; break;
             case SC_OPT_INTEGRAL_FUSE: o.integral_fuse = range(0, 2); regeo = false; break;
             case SC_OPT_INTEGRAL_PRE: o.integral_pre = range(0, 64); regeo = false; break;
-            case SC_OPT_TABLE_U24: o.table_u24 = range(0, 2); regeo = false; break;
             case SC_OPT_CHAIN_WAVES:
                 o.chain_waves = range(0, 16);
                 if (o.chain_waves != 0 && o.chain_waves != 12 && o.chain_waves != 16)

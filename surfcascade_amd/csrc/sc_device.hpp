@@ -16,12 +16,6 @@
 #ifndef SC_SADDR  // 1: corner loads as SGPR base + 32-bit VGPR offset
 #define SC_SADDR 1
 #endif
-#ifndef SC_ABL_U24RAW
-#define SC_ABL_U24RAW 0
-#endif
-#ifndef SC_ABL_VALU_PAD
-#define SC_ABL_VALU_PAD 0
-#endif
 #ifndef SC_LOAD_BARRIER  // 1: every corner load issued before the box sums
 #define SC_LOAD_BARRIER 1
 #endif
@@ -171,74 +165,6 @@ __device__ __forceinline__ void half_box(int shape, const float4 (&cn)[10], f2 (
     else half_box<4, 1>(cn, fh);
 }
 
-// The packed table (launch_pack24): a half-cell's 4 channels as 24-bit
-// integers in 12 B (3 dwords).  `off` is the window origin's byte offset
-// (cell * 12); corner offsets are cells relative to it (|cell| < 2^23).
-struct TabView24 {
-    const char *base;
-    unsigned off;
-    typedef unsigned v3u __attribute__((ext_vector_type(3)));
-    __device__ __forceinline__ v3u at(int cell) const {
-        return *reinterpret_cast<const v3u *>(base + (off + (unsigned)__mul24(cell, 12)));
-    }
-};
-// the 4 fields of a packed half-cell (v_perm_b32 byte gathers)
-__device__ __forceinline__ uint4 unpack24(TabView24::v3u d) {
-    uint4 u;
-    u.x = d.x & 0xffffffu;
-    u.y = __builtin_amdgcn_perm(d.y, d.x, 0x0c050403u);
-    u.z = __builtin_amdgcn_perm(d.z, d.y, 0x0c040302u);
-    u.w = d.z >> 8;
-    return u;
-}
-
-// features_uniform over the packed table: the 10 corner slots of a half as
-// 12-B loads, converted back to the f32 values they hold (exact: integers
-// below 2^24).  Slot 9 is the item's bottom-right corner, its largest value
-// per channel; a lane whose slot 9 holds the 0xffffff marker (some value
-// >= 2^24 - 1) reloads that half's corners from the f32 table.
-template <class P>
-__device__ __forceinline__ void features_uniform24(const TabView24 &T24, const TabView &T, int half_off,
-                                                   const P &pj, f2 (&fp)[16]) {
-    int off[10];
-    corner_offsets(pj, off);
-    f2 h[2][8];
-#pragma unroll
-    for (int hh = 0; hh < 2; hh++) {
-        TabView24::v3u raw[10];
-#pragma unroll
-        for (int m = 0; m < 10; m++) raw[m] = T24.at(hh * half_off + off[m]);
-#if SC_LOAD_BARRIER
-        __builtin_amdgcn_sched_barrier(0);
-#endif
-        float4 cn[10];
-        unsigned mx = 0;
-#pragma unroll
-        for (int m = 0; m < 10; m++) {
-#if SC_ABL_U24RAW  // timing ablation: no unpack / conversion (wrong values)
-            cn[m] = make_float4(__uint_as_float(raw[m].x), __uint_as_float(raw[m].y), __uint_as_float(raw[m].z),
-                                __uint_as_float(raw[m].x ^ raw[m].z));
-            continue;
-#endif
-            const uint4 u = unpack24(raw[m]);
-            if (m == 9) mx = max(max(u.x, u.y), max(u.z, u.w));
-            cn[m] = make_float4((float)u.x, (float)u.y, (float)u.z, (float)u.w);
-        }
-        if (mx == 0xffffffu) {
-#pragma unroll
-            for (int m = 0; m < 10; m++) cn[m] = T.at(hh * half_off + off[m]);
-        }
-        half_box(pj.shape, cn, h[hh]);
-    }
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-        fp[4 * c] = h[0][2 * c];
-        fp[4 * c + 1] = h[0][2 * c + 1];
-        fp[4 * c + 2] = h[1][2 * c];
-        fp[4 * c + 3] = h[1][2 * c + 1];
-    }
-}
-
 // CalcFeature (:379-415) with uniform loads, one half at a time: the 10
 // loads of channels 0-3, their box sums, then the 10 loads of channels 4-7
 // (40 corner registers live instead of 80; measured as fast as all 20 loads
@@ -255,15 +181,6 @@ __device__ __forceinline__ void features_uniform(const TabView &T, int half_off,
         for (int m = 0; m < 10; m++) cn[m] = T.at(hh * half_off + off[m]);
 #if SC_LOAD_BARRIER
         __builtin_amdgcn_sched_barrier(0);
-#endif
-#if SC_ABL_VALU_PAD  // timing ablation: the packed table's unpack VALU on f32 data, results unused
-#pragma unroll
-        for (int m = 0; m < 10; m++) {
-            TabView24::v3u d = {__float_as_uint(cn[m].x), __float_as_uint(cn[m].y), __float_as_uint(cn[m].z)};
-            const uint4 u = unpack24(d);
-            const float a0 = (float)u.x, a1 = (float)u.y, a2 = (float)u.z, a3 = (float)u.w;
-            asm volatile("" ::"v"(a0), "v"(a1), "v"(a2), "v"(a3));
-        }
 #endif
         half_box(pj.shape, cn, h[hh]);
     }
@@ -358,16 +275,6 @@ __device__ __forceinline__ float weak_eval(const TabView &T, int half_off, const
                                            double bias) {
     f2 fp[16];
     descriptor2(T, half_off, pj, fp);
-    return lr_predict2(fp, w4, bias);
-}
-
-// One (window, weak classifier) item over the packed table (f32 fallback).
-template <class P>
-__device__ __forceinline__ float weak_eval24(const TabView24 &T24, const TabView &T, int half_off, const P &pj,
-                                             const float4 *w4, double bias) {
-    f2 fp[16];
-    features_uniform24(T24, T, half_off, pj, fp);
-    normalize2(fp);
     return lr_predict2(fp, w4, bias);
 }
 

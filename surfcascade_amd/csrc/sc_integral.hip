@@ -446,33 +446,7 @@ __global__ __launch_bounds__(64) void colsum_plane_kernel(RowScanArgs a) {
     }
 }
 
-// Packed copy of the table for the chain kernel's gathers: every half-cell
-// (4 channels) in 12 B instead of 16.  A table value below 2^24 - 1 is an
-// integer the f32 holds exactly, so its low 24 bits are a lossless copy (the
-// reader converts back to the same f32); a value >= 2^24 - 1 is stored as
-// 0xffffff, which tells the reader to take the item's corners from the f32
-// table instead (every table channel is non-decreasing in x and y, so an
-// item's largest value is at its bottom-right corner).
-__global__ __launch_bounds__(256) void pack24_kernel(const float4 *__restrict__ t, unsigned *__restrict__ o,
-                                                     long long n4) {
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n4) return;
-    const float4 v = t[i];
-    auto q = [](float f) {  // (padding cells may hold anything: never read)
-        return f >= 16777215.0f ? 0xffffffu : (f > 0.0f ? (unsigned)f : 0u);
-    };
-    const unsigned a = q(v.x), b = q(v.y), c = q(v.z), d = q(v.w);
-    typedef unsigned v3u __attribute__((ext_vector_type(3)));
-    const v3u w = {a | (b << 24), (b >> 8) | (c << 16), (c >> 16) | (d << 8)};
-    *reinterpret_cast<v3u *>(o + 3 * i) = w;
-}
-
 }  // namespace
-
-void launch_pack24(const float4 *table, void *table24, long long n4, hipStream_t s) {
-    hipLaunchKernelGGL(pack24_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, table,
-                       static_cast<unsigned *>(table24), n4);
-}
 
 #ifndef SC_RC_DWORD  // rowcarry4 (dword loads) when the rows start 4-B aligned
 #define SC_RC_DWORD 1

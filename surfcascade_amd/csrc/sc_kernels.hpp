@@ -139,7 +139,6 @@ struct TaskDesc {
 
 struct CascadeArgs {
     const float4 *table;
-    const char *table24;    // chain kernel: the packed 12-B half-cell copy (launch_pack24) or null
     TableGeom g;
     const TaskDesc *tasks;  // [n_bands][kXcds*n_sub]
     const ProjPatch *proj;  // [n_levels][2 parities][K]
@@ -241,8 +240,6 @@ void launch_features(const FeatureArgs &a, hipStream_t s);
 // integral pass 1 (rowcarry4 / rowcarry), sc_integral.hip; returns whether
 // the R rows of frames [0, a.rfull_n) were written (rowcarry4)
 bool launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s);
-// the packed (u24) copy of n4 float4 table cells, 12 B each (chain-kernel gathers)
-void launch_pack24(const float4 *table, void *table24, long long n4, hipStream_t s);
 // two_pass: rowfull + colsum (small batches; rowfull skipped when have_r), else colstrip
 void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s, bool have_r = false);
 // Per-detector launch configuration: the device's CU count (queried once

@@ -271,7 +271,7 @@ struct ItemStats {
     }
 };
 
-template <bool LW, bool RM, class Rows, class Need, class Stats = NoStats, bool U24 = false>
+template <bool LW, bool RM, class Rows, class Need, class Stats = NoStats>
 __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B, const char *Tb,
                                              const float4 *Wl, const double *Bl, const int16_t *Ol,
                                              float *P, float *st_s, unsigned *surv, int8_t *st_p,
@@ -381,14 +381,8 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
                     const unsigned sv = surv[c + i];
                     const TabView Tj{Tb, cell(sv) << 4};
                     const auto pj = B.patch((int)(sv >> 16), (int)(sv & 0xffffu), gk);
-                    if constexpr (U24) {  // gathers from the packed copy (launch_pack24)
-                        const TabView24 T24{a.table24, cell(sv) * 12u};
-                        P[k * G + i] = LW ? weak_eval24(T24, Tj, half_off, pj, Wl + gk * 9, Bl[gk])
-                                          : weak_eval24(T24, Tj, half_off, pj, a.w + gk * 9, a.bias[gk]);
-                    } else {
-                        P[k * G + i] = LW ? weak_eval(Tj, half_off, pj, Wl + gk * 9, Bl[gk])
-                                          : weak_eval(Tj, half_off, pj, a.w + gk * 9, a.bias[gk]);
-                    }
+                    P[k * G + i] = LW ? weak_eval(Tj, half_off, pj, Wl + gk * 9, Bl[gk])
+                                      : weak_eval(Tj, half_off, pj, a.w + gk * 9, a.bias[gk]);
                 }
                 wave_sync();
                 unsigned sv = 0;
@@ -756,7 +750,7 @@ __device__ __forceinline__ void fused_walk(const CascadeArgs &a, const WalkArgs 
 // evaluates ~55 % of the grid's weak items (the visited windows alone are
 // 53 %).  Visited windows that
 // passed every stage are emitted with score (s + S + 1)/S (:201-212).
-template <bool LW, int NW, bool U24>
+template <bool LW, int NW>
 __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkArgs w) {
     constexpr int kChainWaves = NW, kChainThreads = 64 * NW;
     constexpr bool RM = NW > 12;  // rematerialised lane values (128-VGPR budget)
@@ -1120,11 +1114,11 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         wave_sync();
         SC_PROF(c_setup);
 #if SC_PROF_CHAIN
-        eval_windows<LW, RM, SlotRows, decltype(need), ItemStats &, U24>(
-            a, B, reinterpret_cast<const char *>(a.table), Wl, Bl, Ol, P, st_s, surv, st_p, 0, need, istats);
+        eval_windows<LW, RM>(a, B, reinterpret_cast<const char *>(a.table), Wl, Bl, Ol, P, st_s, surv,
+                         st_p, 0, need, istats);
 #else
-        eval_windows<LW, RM, SlotRows, decltype(need), NoStats, U24>(
-            a, B, reinterpret_cast<const char *>(a.table), Wl, Bl, Ol, P, st_s, surv, st_p, 0, need);
+        eval_windows<LW, RM>(a, B, reinterpret_cast<const char *>(a.table), Wl, Bl, Ol, P, st_s, surv,
+                         st_p, 0, need);
 #endif
         wave_sync();
         SC_PROF(c_eval);
@@ -1383,19 +1377,26 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hi
     if (c.lds_weights >= 0) lw = lw && c.lds_weights != 0;  // SC_OPT_LDS_WEIGHTS
     const size_t lds = model_lds_bytes(a.K, lw) + scratch(nw);
     const int nt = 64 * nw;
-    // the variant: (weights in LDS, waves, gathers from the packed table)
-    const int v = (lw ? 1 : 0) | (nw == 16 ? 2 : 0) | (a.table24 ? 4 : 0);
-    using K = void (*)(CascadeArgs, WalkArgs);
-    static const K kern[8] = {chain_kernel<false, 12, false>, chain_kernel<true, 12, false>,
-                              chain_kernel<false, 16, false>, chain_kernel<true, 16, false>,
-                              chain_kernel<false, 12, true>,  chain_kernel<true, 12, true>,
-                              chain_kernel<false, 16, true>,  chain_kernel<true, 16, true>};
     int per_cu = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern[v], nt, lds);
+    if (nw == 16 && lw)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<true, 16>, nt, lds);
+    else if (nw == 16)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<false, 16>, nt, lds);
+    else if (lw)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<true, 12>, nt, lds);
+    else
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<false, 12>, nt, lds);
     per_cu = std::max(1, std::min(per_cu, 4));
     if (c.wgs_per_cu > 0) per_cu = std::min(per_cu, c.wgs_per_cu);  // SC_OPT_WGS_PER_CU
     const int grid = std::max(1, c.cus) * per_cu;
-    hipLaunchKernelGGL(kern[v], dim3(grid), dim3(nt), lds, s, a, w);
+    if (nw == 16 && lw)
+        hipLaunchKernelGGL((chain_kernel<true, 16>), dim3(grid), dim3(nt), lds, s, a, w);
+    else if (nw == 16)
+        hipLaunchKernelGGL((chain_kernel<false, 16>), dim3(grid), dim3(nt), lds, s, a, w);
+    else if (lw)
+        hipLaunchKernelGGL((chain_kernel<true, 12>), dim3(grid), dim3(nt), lds, s, a, w);
+    else
+        hipLaunchKernelGGL((chain_kernel<false, 12>), dim3(grid), dim3(nt), lds, s, a, w);
     return grid;
 }
 
