@@ -221,9 +221,47 @@ __device__ __forceinline__ void descriptor2(const TabView &T, int half_off, cons
     normalize2(fp);
 }
 
+#ifndef SC_SHORT_RN  // sqrt / reciprocal of Normalize without the range-end steps (same bits in its range)
+#define SC_SHORT_RN 1
+#endif
+// IEEE sqrt for x in [2^-96, FLT_MAX]: the compiler's correctly rounded
+// sequence (v_sqrt_f32, then the two FMA residual checks one ulp either
+// side) without its scaling of x < 2^-96 and its 0 / inf / NaN class select,
+// which never act in that range.  Normalize's sums of squares are >=
+// FLT_EPSILON (the seed) and finite (box sums < 2^32).
+__device__ __forceinline__ float sqrt_rn(float x) {
+#if SC_SHORT_RN
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = fmaf(-sd, s, x) <= 0.0f ? sd : s;
+    r = fmaf(-su, s, x) > 0.0f ? su : r;
+    return r;
+#else
+    return sqrtf(x);
+#endif
+}
+// IEEE 1/d for d in [2^-20, 2^40]: the compiler's division sequence (reciprocal,
+// refinement, two FMA corrections) without v_div_scale / v_div_fmas scaling
+// and v_div_fixup, which act only for operands near the exponent range's
+// ends or special values.  Normalize's d = sqrt(SS) is in [3.4e-4, 2^36].
+__device__ __forceinline__ float rcp_rn(float d) {
+#if SC_SHORT_RN
+    float r = __builtin_amdgcn_rcpf(d);
+    const float e = fmaf(-d, r, 1.0f);
+    r = fmaf(e, r, r);
+    float q = 1.0f * r;
+    const float e2 = fmaf(-d, q, 1.0f);
+    q = fmaf(e2, r, q);
+    const float e3 = fmaf(-d, q, 1.0f);
+    return fmaf(e3, r, q);
+#else
+    return 1.0f / d;
+#endif
+}
+
 __device__ __forceinline__ void normalize2(f2 (&fp)[16]) {
     const float theta = 0.35355338f;  // 2/sqrt(32.f) (.h:36)
-    const float t = sqrtf(ss_hadd2(fp)) * theta, nt = -t;
+    const float t = sqrt_rn(ss_hadd2(fp)) * theta, nt = -t;
     // _mm_max_ps(_mm_min_ps(f, t), -t) as one v_med3_f32: identical bits here
     // because f is a finite box sum (never NaN, never -0) and t > 0 (SS >= eps)
 #pragma unroll
@@ -231,7 +269,7 @@ __device__ __forceinline__ void normalize2(f2 (&fp)[16]) {
         fp[j].x = __builtin_amdgcn_fmed3f(fp[j].x, nt, t);
         fp[j].y = __builtin_amdgcn_fmed3f(fp[j].y, nt, t);
     }
-    const float r = 1.0f / sqrtf(ss_hadd2(fp));
+    const float r = rcp_rn(sqrt_rn(ss_hadd2(fp)));
 #pragma unroll
     for (int j = 0; j < 16; j++) fp[j] = fp[j] * f2{r, r};
 }
