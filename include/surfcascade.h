@@ -191,6 +191,13 @@ int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, 
 #define SC_INFO_VISITED 5       /* windows the adaptive stride visited (last) */
 #define SC_INFO_FUSED_FRAMES 6  /* frames of the last call whose integral      */
                                 /* column walks ran inside the chain kernel    */
+#define SC_INFO_CHAIN_WAVES 7   /* waves per workgroup of the last chain-kernel */
+                                /* launch (12 or 16; 0: none yet)              */
+#define SC_INFO_COLUMN_PASS 8   /* the last call's integral column pass for the */
+                                /* frames built outside the chain kernel:      */
+                                /* 1 two-pass (rowcarry R + colsum), 2 colstrip */
+#define SC_INFO_SPEC_ROUNDS 9   /* speculative evaluation rounds of the last    */
+                                /* chain launch (one-frame launches only)      */
 int sc_detector_info(sc_detector *d, int what, int64_t *value);
 
 /* ---- tuning and test options ---------------------------------------------
@@ -198,8 +205,9 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
  * (tests/test_gpu_parity.py runs each against the oracle); the defaults are
  * the measured-fastest.  Options 15-16 restrict the scan to a range of levels
  * (profiling of level groups): they DO change the result, to the windows of
- * those levels.  The library reads no environment variable: these are set per
- * detector, explicitly. */
+ * those levels.  Option 20 is a test hook (a deliberately lost hand-off:
+ * the call must fail, tests/test_gpu_parity.py).  The library reads no
+ * environment variable: these are set per detector, explicitly. */
 #define SC_OPT_FULL_GRID 1    /* 1: evaluate every grid window (cascade + walk   */
                               /* kernels) instead of the lazy chain kernel (0) */
 #define SC_OPT_CHUNK_MIN 2    /* stages with >= this many survivors run one lane */
@@ -234,6 +242,12 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
                               /* launch has 2+ frames                          */
 #define SC_OPT_INTEGRAL_PRE 19 /* fused: frames per launch integrated before   */
                               /* the chain kernel (0: default 2)               */
+#define SC_OPT_TEST_DROP_HANDOFF 20 /* test only (-1 off): the chain kernel drops */
+                              /* the segment-0 hand-off of row task `value`  */
+                              /* of every launch; the watchdog must then     */
+                              /* raise SC_ERR_DEVICE at the next sync.  Only */
+                              /* the test-hook build (lib/testhooks) accepts */
+                              /* a value other than -1                       */
 int sc_detector_set_option(sc_detector *d, int option, int64_t value);
 
 /* Enable per-window debug records (grid order) for the next detect calls. */
@@ -304,6 +318,23 @@ int sc_decode_jpeg_gray(const uint8_t *data, size_t len, uint8_t *out,
                         size_t cap, int *w, int *h);
 int sc_imread_gray(const char *path, uint8_t *out, size_t cap, int *w,
                    int *h);
+
+/* ---- device self-check of the Normalize arithmetic ----------------------
+ * The item loop's Normalize (DenseSURFFeatureExtractor.cpp:427-457) uses a
+ * shortened IEEE sqrt and reciprocal (sc_device.hpp sqrt_rn / rcp_rn).  This
+ * runs every f32 bit pattern in [lo_bits, hi_bits] through the short
+ * sequence (op 0: sqrt, 1: reciprocal), the compiler's full IEEE sequence and
+ * the f64 route on GPU `device`; out[0] = patterns differing from the full
+ * sequence, out[1] = from the f64 route, out[2] = patterns checked, out[3] =
+ * the smallest differing pattern (UINT64_MAX: none).  Test support: the
+ * detect path does not call it. */
+int sc_selftest_rn(int device, int op, uint32_t lo_bits, uint32_t hi_bits,
+                   uint64_t out[4]);
+/* Operand ranges Normalize can produce for the largest accepted frame
+ * (|box sum| <= 2*255*W*H): ss[0..1] bounds SS and SS2, d[0..1] bounds
+ * sqrt(SS2); the frame limits of sc_detect* keep these inside the ranges
+ * sc_selftest_rn is run over (tests/test_gpu_rn.py). */
+void sc_normalize_operand_range(int max_w, int max_h, double ss[2], double d[2]);
 
 const char *sc_last_error(void);
 const char *sc_version(void);

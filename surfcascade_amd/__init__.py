@@ -48,7 +48,8 @@ OPTIONS = {"full_grid": 1, "chunk_min": 2, "table_layout": 3, "phases": 4, "subs
            "band_rows": 6, "row_order": 7, "row_block": 8, "chain_chunk": 9, "lds_weights": 10,
            "wgs_per_cu": 11, "profile": 12, "chain_segs": 13, "integral_passes": 14,
            "level_lo": 15, "level_hi": 16, "chain_waves": 17,
-           "integral_fuse": 18, "integral_pre": 19}
+           "integral_fuse": 18, "integral_pre": 19,
+           "test_drop_handoff": 20}
 
 # every symbol include/surfcascade.h declares
 EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_model_save",
@@ -60,7 +61,7 @@ EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_mode
            "sc_detector_set_shard", "sc_detector_set_option", "sc_detector_set_debug", "sc_debug_dump", "sc_set_timing", "sc_get_timing",
            "sc_group_rectangles", "sc_group_detections", "sc_fddb_format",
            "sc_miner_create", "sc_mine", "sc_mine_device", "sc_mine_batch", "sc_mine_batch_device", "sc_fast_nms", "sc_decode_jpeg_gray", "sc_imread_gray",
-           "sc_last_error", "sc_version")
+           "sc_selftest_rn", "sc_normalize_operand_range", "sc_last_error", "sc_version")
 
 
 class SurfCascadeError(RuntimeError):
@@ -165,6 +166,9 @@ def load_library():
     L.sc_fast_nms.argtypes = [vp, i32, ctypes.c_double, vp, i32, P(i32)]
     L.sc_decode_jpeg_gray.argtypes = [vp, sz, vp, sz, P(i32), P(i32)]
     L.sc_imread_gray.argtypes = [ctypes.c_char_p, vp, sz, P(i32), P(i32)]
+    L.sc_selftest_rn.argtypes = [i32, i32, ctypes.c_uint32, ctypes.c_uint32, P(ctypes.c_uint64)]
+    L.sc_normalize_operand_range.argtypes = [i32, i32, P(ctypes.c_double), P(ctypes.c_double)]
+    L.sc_normalize_operand_range.restype = None
     _lib = L
     return L
 
@@ -173,6 +177,27 @@ def _check(rc):
     if rc < 0:
         raise SurfCascadeError(rc, load_library().sc_last_error().decode(errors="replace"))
     return rc
+
+
+def selftest_rn(op, lo_bits, hi_bits, device=0):
+    """Exhaustive device check of the short IEEE sqrt (op 0) / reciprocal
+    (op 1) Normalize uses (sc_selftest_rn): every f32 pattern in
+    [lo_bits, hi_bits].  Returns (differs_from_full, differs_from_f64,
+    checked, first_bad or None)."""
+    L = load_library()
+    out = (ctypes.c_uint64 * 4)()
+    _check(L.sc_selftest_rn(device, op, lo_bits, hi_bits, out))
+    return int(out[0]), int(out[1]), int(out[2]), (None if out[3] == 2**64 - 1 else int(out[3]))
+
+
+def normalize_operand_range(max_w, max_h):
+    """((ss_lo, ss_hi), (d_lo, d_hi)): Normalize's sqrt / reciprocal operand
+    bounds for frames up to max_w x max_h (sc_normalize_operand_range)."""
+    L = load_library()
+    ss = (ctypes.c_double * 2)()
+    d = (ctypes.c_double * 2)()
+    L.sc_normalize_operand_range(max_w, max_h, ss, d)
+    return (ss[0], ss[1]), (d[0], d[1])
 
 
 def extract_patches(tmpl_w=40, tmpl_h=40):
@@ -501,7 +526,8 @@ class Detector:
 
     # -- introspection ---------------------------------------------------------
     def info(self, key):
-        keys = {"levels": 1, "grid_windows": 2, "rows": 3, "table_pitch": 4, "visited": 5, "fused_frames": 6}
+        keys = {"levels": 1, "grid_windows": 2, "rows": 3, "table_pitch": 4, "visited": 5, "fused_frames": 6,
+                "chain_waves": 7, "column_pass": 8, "spec_rounds": 9}
         v = ctypes.c_int64()
         _check(load_library().sc_detector_info(self._h, keys[key], ctypes.byref(v)))
         return v.value

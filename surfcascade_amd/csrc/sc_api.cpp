@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -130,6 +131,7 @@ struct sc_detector {
         int chain_waves = 0;             // chain kernel waves per workgroup (0 auto)
         int integral_fuse = 0;           // column walks inside the chain kernel: 0 auto, 1 never, 2 from 2 frames
         int integral_pre = 0;            // fused: frames integrated before the chain kernel (0: 2)
+        int drop_handoff = -1;           // test only: task whose segment-0 hand-off is dropped (watchdog)
     } opt;
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
@@ -158,7 +160,14 @@ struct sc_detector {
     DevBuf<int> d_queues;       // per-XCD task counters of the cascade kernel
     DevBuf<int> d_entry;        // chain kernel: per (row, segment) chain entry + 1
     DevBuf<unsigned long long> d_prof;  // chain kernel phase cycles (SC_PROF_CHAIN builds)
-    long long err_word = -1;    // chain kernel: index of the hand-off watchdog word in d_entry
+    long long err_word = -1;    // chain kernel: index of the launch's watchdog-fired flag in d_entry
+    long long spec_word = -1;   // ... and of its speculative-round count (SC_INFO_SPEC_ROUNDS)
+    // chain kernel: hand-offs that timed out, summed over every launch since
+    // the last check_chain (sticky: rowcarry's per-call zeroing does not
+    // touch it, so a timeout in any pipelined step is still raised at the
+    // next synchronisation); zeroed once at allocation and after each read
+    DevBuf<int> d_err;
+    bool chain_launched = false;  // a chain launch since the last check_chain
     DevBuf<int8_t> d_st_p;      // per grid window: stage reached (-1 prefilter reject)
     DevBuf<float> d_st_s;       // per grid window: last stage score
     // debug
@@ -167,6 +176,8 @@ struct sc_detector {
     int last_frames = 0;
     int last_fused = 0;  // frames of the last call integrated inside the chain kernel
     int last_nseg = 8;   // segments per row of the last chain launch (profiling readout)
+    int last_waves = 0;  // waves per workgroup of the last chain launch (SC_INFO_CHAIN_WAVES)
+    int last_colpass = 0;  // column pass of the last call's prebuilt frames (SC_INFO_COLUMN_PASS)
     // timing
     bool timing = false;
     struct Pending {
@@ -192,7 +203,7 @@ struct sc_detector {
         d_proj_all.release(); d_mine_cnt.release(); d_mine_off.release(); d_mine_win.release();
         d_feat.release();
         d_frames.release(); d_table.release(); d_carry.release(); d_out.release(); d_counters.release();
-        d_visited.release(); d_queues.release(); d_entry.release(); d_st_p.release(); d_st_s.release();
+        d_visited.release(); d_queues.release(); d_entry.release(); d_err.release(); d_st_p.release(); d_st_s.release();
         d_dbg_v.release(); d_prof.release();
         h_stage.release();
         if (stream) (void)hipStreamDestroy(stream);
@@ -223,6 +234,21 @@ int ref_levels(int W, int H, const sc_scan_params &p) {
     double a = std::log((float)W / (float)p.base_len) / std::log(p.scale_factor);
     double b = std::log((float)H / (float)(p.base_len * p.aspect_h)) / std::log(p.scale_factor);
     return (int)std::min(a, b) + 1;
+}
+
+// Operand ranges of Normalize's sqrt / reciprocal (DenseSURFFeatureExtractor.cpp:
+// 427-457) for a W x H frame: a channel's table value is at most 255*W*H (the
+// f32 sums round to at most that bound's next representable value), a box
+// sum (TL + BR) - (TR + BL) at most twice that, so SS = eps + sum of 32
+// squares <= eps + 32 * (2 * 255 * W * H)^2 (with a 1e-6 relative margin for
+// the f32 roundings); SS >= eps (FLT_EPSILON seed, non-negative terms); the
+// clipped SS2 lies between eps and SS.  d = sqrt(SS2).
+void normalize_operand_range(int W, int H, double ss[2], double d[2]) {
+    const double fmax = 2.0 * 255.0 * (double)W * (double)H * (1.0 + 1e-6);
+    ss[0] = (double)FLT_EPSILON;
+    ss[1] = ((double)FLT_EPSILON + 32.0 * fmax * fmax) * (1.0 + 1e-6);
+    d[0] = std::sqrt(ss[0]) * (1.0 - 1e-6);
+    d[1] = std::sqrt(ss[1]);
 }
 
 void build_geometry(sc_detector *d, int W, int H) {
@@ -259,6 +285,14 @@ void build_geometry(sc_detector *d, int W, int H) {
         t.frame4 = (long long)(H + 1) * t.rowp;
         if ((long long)(H + 1) * t.rowp > (1ll << 28))  // byte offsets within a frame table: u32
             throw Error{SC_ERR_INVALID, "frame too large for 32-bit table offsets"};
+        {   // Normalize's operands stay inside the ranges the short sqrt /
+            // reciprocal were checked over exhaustively (sc_device.hpp,
+            // tests/test_gpu_rn.py); never fires for a frame the offset check admits
+            double ss[2], dd[2];
+            normalize_operand_range(W, H, ss, dd);
+            if (ss[0] < sc::kRnSqrtLo || ss[1] > sc::kRnSqrtHi || dd[0] < sc::kRnRcpLo || dd[1] > sc::kRnRcpHi)
+                throw Error{SC_ERR_INVALID, "frame too large for Normalize's checked operand range"};
+        }
         // x / ph as umulhi(x, ceil(2^32/ph)) in the chain kernel's per-item
         // projection: exact for every column a patch corner can take
         t.phm = t.ph > 1 ? (unsigned)((0x100000000ull + (unsigned)t.ph - 1) / (unsigned)t.ph) : 0u;
@@ -608,10 +642,17 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     const size_t n_rows = g.rows.size();
     const bool chain = n_rows > 0 && lazy && !d->miner;
     // hand-off words of a chain launch: [rows x frames x kXcds] entries, the
-    // watchdog word, then the fused integral's walk counter and per-frame
-    // walk counts (WalkArgs::int_ctl); sized for the largest launch
-    auto entry_words = [&](int frames) { return (long long)n_rows * frames * sc::kXcds + 2 + frames; };
-    if (chain) d->d_entry.ensure((size_t)entry_words(std::min(chunk, n)));
+    // watchdog-fired flag, the fused integral's walk counter and per-frame
+    // walk counts (WalkArgs::int_ctl), the speculative-round count; sized
+    // for the largest launch
+    auto entry_words = [&](int frames) { return (long long)n_rows * frames * sc::kXcds + 3 + frames; };
+    if (chain) {
+        d->d_entry.ensure((size_t)entry_words(std::min(chunk, n)));
+        if (!d->d_err.p) {
+            d->d_err.ensure(1);
+            HIPCHK(hipMemsetAsync(d->d_err.p, 0, sizeof(int), d->stream));
+        }
+    }
     // Fused integral (SC_OPT_INTEGRAL_FUSE): the first `pre` frames of every
     // launch are integrated by their own kernels (2 by default: a frame's 60
     // walks inside the chain kernel take longer than the chain takes over
@@ -676,6 +717,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     } else {
         sc::launch_colscan(ra, n, two_pass_all, d->stream, have_r);
     }
+    d->last_colpass = (fuse ? two_pass_pre : two_pass_all) ? 1 : 2;
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_COLSCAN, e0);
 
@@ -750,8 +792,12 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             wc.row_visited = d->d_visited.p + (size_t)f0 * n_rows;
             wc.entry = d->d_entry.p;
             d->err_word = (long long)(n_rows * std::min(chunk, n) * sc::kXcds);
-            wc.err = d->d_entry.p + d->err_word;
-            wc.int_ctl = wc.err + 1;
+            wc.fired = d->d_entry.p + d->err_word;  // per launch: zeroed with the entries
+            wc.err = d->d_err.p;                    // sticky over launches and calls
+            wc.int_ctl = wc.fired + 1;
+            wc.spec = wc.int_ctl + 1 + std::min(chunk, n);
+            d->spec_word = wc.spec - d->d_entry.p;
+            d->chain_launched = true;
             if (fuse && nc > pre) {
                 wc.frames = d_frames + (long long)f0 * H * stride;
                 wc.frame_bytes = (long long)H * stride;
@@ -763,6 +809,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
                 d->last_fused += nc - pre;
             }
             wc.frame0 = f0;
+            wc.drop_task1 = d->opt.drop_handoff + 1;  // SC_OPT_TEST_DROP_HANDOFF (0: none)
             wc.nseg = segs_for(nc);
             d->last_nseg = wc.nseg;
             wc.seg_shift = wc.nseg == 8 ? 0 : wc.nseg == 4 ? 1 : wc.nseg == 2 ? 2 : 3;
@@ -776,12 +823,11 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
                 wc.prof = d->d_prof.p;
             }
             if (f0 > 0) {  // (the first chunk's were cleared by rowcarry)
-                // (the watchdog word between them keeps counting over the launches)
                 HIPCHK(hipMemsetAsync(d->d_entry.p, 0, sizeof(int) * n_rows * nc * sc::kXcds, d->stream));
-                HIPCHK(hipMemsetAsync(wc.int_ctl, 0, sizeof(int) * (size_t)(1 + nc), d->stream));
+                HIPCHK(hipMemsetAsync(wc.fired, 0, sizeof(int) * (size_t)(3 + std::min(chunk, n)), d->stream));  // + int_ctl, spec
                 HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kQueueWords, d->stream));
             }
-            sc::launch_chain(cc, wc, launch_cfg(d), d->stream);
+            sc::launch_chain(cc, wc, launch_cfg(d), d->stream, &d->last_waves);
             HIPCHK(hipGetLastError());
         }
         timed_end(d, SC_KERNEL_WINDOWS, e0);
@@ -793,12 +839,17 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     timed_end(d, SC_KERNEL_WALK, e0);
 }
 
-// The chain kernel's hand-off watchdog (reads after the stream has drained).
+// The chain kernel's hand-off watchdog (reads after the stream has drained):
+// every launch since the last check, pipelined steps included.
 void check_chain(sc_detector *d) {
-    if (!d->lazy || d->err_word < 0) return;
+    if (!d->lazy || !d->chain_launched || !d->d_err.p) return;
+    d->chain_launched = false;
     int err = 0;
-    HIPCHK(hipMemcpy(&err, d->d_entry.p + d->err_word, sizeof(int), hipMemcpyDeviceToHost));
-    if (err) throw Error{SC_ERR_DEVICE, "chain kernel: " + std::to_string(err) + " segment hand-off(s) timed out"};
+    HIPCHK(hipMemcpy(&err, d->d_err.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (err) {
+        HIPCHK(hipMemset(d->d_err.p, 0, sizeof(int)));
+        throw Error{SC_ERR_DEVICE, "chain kernel: " + std::to_string(err) + " segment hand-off(s) timed out"};
+    }
     if (d->d_prof.p) {
         unsigned long long pc[16];
         HIPCHK(hipMemcpy(pc, d->d_prof.p, sizeof(pc), hipMemcpyDeviceToHost));
@@ -1425,6 +1476,19 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value) {
         case SC_INFO_ROWS: *value = (int64_t)d->geo.rows.size(); break;
         case SC_INFO_TABLE_PITCH: *value = d->geo.tg.rowp; break;
         case SC_INFO_FUSED_FRAMES: *value = d->last_fused; break;
+        case SC_INFO_CHAIN_WAVES: *value = d->last_waves; break;
+        case SC_INFO_COLUMN_PASS: *value = d->last_colpass; break;
+        case SC_INFO_SPEC_ROUNDS:  // the last chain launch's speculative rounds
+            return guarded([&] {
+                int v = 0;
+                if (d->spec_word >= 0) {
+                    HIPCHK(hipSetDevice(d->device));
+                    HIPCHK(hipStreamSynchronize(d->stream));
+                    HIPCHK(hipMemcpy(&v, d->d_entry.p + d->spec_word, sizeof(int), hipMemcpyDeviceToHost));
+                }
+                *value = v;
+                return SC_OK;
+            });
         case SC_INFO_VISITED: {  // sum of the walk kernel's per-row counts
             return guarded([&] {
                 HIPCHK(hipSetDevice(d->device));
@@ -1483,6 +1547,13 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
             case SC_OPT_INTEGRAL_PASSES: o.integral_passes = range(0, 2); regeo = false; break;
             case SC_OPT_INTEGRAL_FUSE: o.integral_fuse = range(0, 2); regeo = false; break;
             case SC_OPT_INTEGRAL_PRE: o.integral_pre = range(0, 64); regeo = false; break;
+            case SC_OPT_TEST_DROP_HANDOFF:
+#if !defined(SC_TEST_HOOKS) || !SC_TEST_HOOKS
+                if (value != -1) throw Error{SC_ERR_INVALID, "test_drop_handoff needs the test-hook build (lib/testhooks)"};
+#endif
+                o.drop_handoff = range(-1, INT32_MAX - 1);
+                regeo = false;
+                break;
             case SC_OPT_CHAIN_WAVES:
                 o.chain_waves = range(0, 16);
                 if (o.chain_waves != 0 && o.chain_waves != 12 && o.chain_waves != 16)
@@ -1588,6 +1659,36 @@ int sc_get_timing(sc_detector *d, double ms[SC_KERNEL_COUNT], int64_t n[SC_KERNE
         }
         return SC_OK;
     });
+}
+
+int sc_selftest_rn(int device, int op, uint32_t lo, uint32_t hi, uint64_t out[4]) {
+    return guarded([&] {
+        if (!out || (op != 0 && op != 1) || hi < lo) throw Error{SC_ERR_INVALID, "bad self-test arguments"};
+        int ndev = 0;
+        HIPCHK(hipGetDeviceCount(&ndev));
+        if (device < 0 || device >= ndev) throw Error{SC_ERR_DEVICE, "device not present"};
+        HIPCHK(hipSetDevice(device));
+        int cus = 0;
+        HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        unsigned long long *d_out = nullptr;
+        HIPCHK(hipMalloc(&d_out, 4 * sizeof(unsigned long long)));
+        const unsigned long long init[4] = {0, 0, 0, ~0ull};
+        int rc = SC_OK;
+        if (hipMemcpy(d_out, init, sizeof(init), hipMemcpyHostToDevice) != hipSuccess) rc = SC_ERR_DEVICE;
+        if (rc == SC_OK) {
+            sc::launch_rn_check(op, lo, hi, d_out, cus, nullptr);
+            if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+                hipMemcpy(out, d_out, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+                rc = SC_ERR_DEVICE;
+        }
+        (void)hipFree(d_out);
+        if (rc != SC_OK) throw Error{rc, "self-test kernel failed"};
+        return SC_OK;
+    });
+}
+
+void sc_normalize_operand_range(int max_w, int max_h, double ss[2], double d[2]) {
+    normalize_operand_range(max_w, max_h, ss, d);
 }
 
 }  // extern "C"

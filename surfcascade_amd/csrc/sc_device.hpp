@@ -224,11 +224,18 @@ __device__ __forceinline__ void descriptor2(const TabView &T, int half_off, cons
 #ifndef SC_SHORT_RN  // sqrt / reciprocal of Normalize without the range-end steps (same bits in its range)
 #define SC_SHORT_RN 1
 #endif
-// IEEE sqrt for x in [2^-96, FLT_MAX]: the compiler's correctly rounded
-// sequence (v_sqrt_f32, then the two FMA residual checks one ulp either
-// side) without its scaling of x < 2^-96 and its 0 / inf / NaN class select,
-// which never act in that range.  Normalize's sums of squares are >=
-// FLT_EPSILON (the seed) and finite (box sums < 2^32).
+// Ranges (the same constants as kRnSqrt* / kRnRcp* in sc_kernels.hpp).
+// Normalize's operands for any frame the API accepts: SS, SS2 in
+// [FLT_EPSILON, 2^77] (the FLT_EPSILON seed; |box sum| <= 2*255*W*H < 2^36
+// with W*H < 2^27, so 32 squares < 2^77), d = sqrt(SS2) in [2^-11.5, 2^38.5]
+// (build_geometry checks it: normalize_operand_range).  The sequences below
+// are stated for the wider ranges sqrt_rn: x in [2^-96, FLT_MAX] and
+// rcp_rn: d in [2^-20, 2^40], and tests/test_gpu_rn.py compares them with
+// the full IEEE sequences and the f64 route for EVERY f32 in those ranges
+// (sc_selftest_rn).
+// sqrt_rn: the compiler's correctly rounded sequence (v_sqrt_f32, then the
+// two FMA residual checks one ulp either side) without its scaling of
+// x < 2^-96 and its 0 / inf / NaN class select, which never act in its range.
 __device__ __forceinline__ float sqrt_rn(float x) {
 #if SC_SHORT_RN
     const float s = __builtin_amdgcn_sqrtf(x);
@@ -240,10 +247,10 @@ __device__ __forceinline__ float sqrt_rn(float x) {
     return sqrtf(x);
 #endif
 }
-// IEEE 1/d for d in [2^-20, 2^40]: the compiler's division sequence (reciprocal,
-// refinement, two FMA corrections) without v_div_scale / v_div_fmas scaling
-// and v_div_fixup, which act only for operands near the exponent range's
-// ends or special values.  Normalize's d = sqrt(SS) is in [3.4e-4, 2^36].
+// rcp_rn: the compiler's division sequence for 1/d (reciprocal, refinement,
+// two FMA corrections) without v_div_scale / v_div_fmas scaling and
+// v_div_fixup, which act only for operands near the exponent range's ends or
+// special values, never in its range.
 __device__ __forceinline__ float rcp_rn(float d) {
 #if SC_SHORT_RN
     float r = __builtin_amdgcn_rcpf(d);

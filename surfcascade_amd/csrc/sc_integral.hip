@@ -128,19 +128,29 @@ __global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
         for (int i = lane; i < g.rowp; i += 64) tab[i] = z4;
     if (lane < 2) tab[(long long)(y + 1) * g.rowp + lane * g.hs] = z4;  // column 0
 
-    const uint32_t *ru = reinterpret_cast<const uint32_t *>(img + (long long)(y > 0 ? y - 1 : 0) * a.stride);
-    const uint32_t *rc = reinterpret_cast<const uint32_t *>(img + (long long)y * a.stride);
-    const uint32_t *rd = reinterpret_cast<const uint32_t *>(img + (long long)(y < H - 1 ? y + 1 : H - 1) * a.stride);
+    const uint8_t *ru = img + (long long)(y > 0 ? y - 1 : 0) * a.stride;
+    const uint8_t *rc = img + (long long)y * a.stride;
+    const uint8_t *rd = img + (long long)(y < H - 1 ? y + 1 : H - 1) * a.stride;
     uint4 *out = reinterpret_cast<uint4 *>(a.carry) + ((long long)frame * H + y) * ns * 2;
     const int np = (W + 255) / 256;
+    // a row's dword at x0 (4-B aligned: frame and stride are); the row's last
+    // partial dword byte by byte, so no load reads past column W - 1 (a
+    // device caller's buffer may end at the last row's W-th byte).  The bytes
+    // past W read as 0 and are never used (x = W - 1 clamps x + 1 to itself).
+    auto ld4 = [&](const uint8_t *row, int x0) -> uint32_t {
+        if (x0 + 4 <= W) return *reinterpret_cast<const uint32_t *>(row + x0);
+        uint32_t v = 0u;
+        for (int k = 0; k < 4 && x0 + k < W; k++) v |= (uint32_t)row[x0 + k] << (8 * k);
+        return v;
+    };
     // a pass's dwords (rows u, c, d), loaded one pass ahead
     auto load = [&](int p, uint32_t &u, uint32_t &c, uint32_t &d) {
         const int x0 = p * 256 + 4 * lane;
         u = c = d = 0u;
-        if (p < np && x0 < W) {  // (stride % 4 == 0: the dword stays inside the row's pitch)
-            u = ru[x0 >> 2];
-            c = rc[x0 >> 2];
-            d = rd[x0 >> 2];
+        if (p < np && x0 < W) {
+            u = ld4(ru, x0);
+            c = ld4(rc, x0);
+            d = ld4(rd, x0);
         }
     };
     uint32_t u0, c0, d0;

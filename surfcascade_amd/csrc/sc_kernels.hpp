@@ -177,7 +177,10 @@ struct WalkArgs {
     uint8_t *dbg_v;  // optional [frame][grid] visited flags
     int row_max;     // chain kernel: most windows in one row segment (LDS sizing)
     int *entry;      // chain kernel: [frame*rows][kXcds] chain entry + 1 per segment (zeroed)
-    int *err;        // chain kernel: hand-off timeouts (must stay 0)
+    int *err;        // chain kernel: hand-off timeouts, summed over launches and calls (must stay 0)
+    int *fired;      // chain kernel: this launch's watchdog has fired (zeroed per launch)
+    int *spec;       // chain kernel: speculative rounds of this launch (zeroed per launch)
+    int drop_task1;  // test only: row task + 1 whose segment-0 hand-off is dropped (0: none)
     int frame0;      // chain kernel: first frame of this launch (record frame index)
     int nseg;        // chain kernel: segments per row (8; 4 for one-frame launches)
     int seg_shift;   // chain kernel: log2(kXcds / nseg)
@@ -257,7 +260,15 @@ void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s);
 // Lazy grid: the walk drives the cascade (chain kernel, sc_windows.hip); the
 // cascade args' st_p / st_s, when not null, receive the evaluated windows
 // (others keep the caller's fill).  Returns the number of workgroups.
-int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hipStream_t s);
+int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hipStream_t s,
+                 int *waves_out = nullptr);  // waves_out: the workgroup's waves (12 / 16)
+// sc_selftest.hip: exhaustive sqrt_rn / rcp_rn check (sc_selftest_rn).  The
+// ranges the shortened sequences are stated for (sc_device.hpp) and checked
+// over bit pattern by bit pattern (tests/test_gpu_rn.py); build_geometry
+// rejects a frame whose Normalize operands could leave them.
+constexpr double kRnSqrtLo = 0x1p-96, kRnSqrtHi = 0x1.fffffep127;  // sqrt_rn: [2^-96, FLT_MAX]
+constexpr double kRnRcpLo = 0x1p-20, kRnRcpHi = 0x1p40;            // rcp_rn: [2^-20, 2^40]
+void launch_rn_check(int op, uint32_t lo, uint32_t hi, unsigned long long *out, int cus, hipStream_t s);
 size_t chain_lds_bytes(int K, int seg_max, int n_levels);
 size_t cascade_lds_bytes(int K, int strip_max, int band_rows);
 

@@ -45,6 +45,10 @@ namespace {
 #endif
 
 
+#ifndef SC_TEST_HOOKS  // 1: test-hook library (lib/testhooks): SC_OPT_TEST_DROP_HANDOFF acts
+#define SC_TEST_HOOKS 0
+#endif
+
 #ifndef SC_ABL_NOWAIT  // timing ablation only: segments start without the hand-off (wrong results)
 #define SC_ABL_NOWAIT 0
 #endif
@@ -80,6 +84,21 @@ __device__ __forceinline__ int lane_id() {
     } else {
         return threadIdx.x & 63;
     }
+}
+
+// The wave's lead lane: the first ACTIVE lane (v_mbcnt over the current exec
+// mask).  Every "one lane does it, readfirstlane broadcasts it" site of the
+// chain kernel uses it, so the lane that performs the atomic / load / store
+// is by construction the lane readfirstlane reads, whatever the exec mask.
+// The earlier form (lane_id() == 0, with the 12-wave kernel's lane-0 mask
+// hoisted into an SGPR pair before the walker loop) is correct only while
+// lane 0 is active at every such site; a dequeue whose atomic lane is
+// inactive returns task 0 forever (readfirstlane then reads a lane that
+// never did the atomic): the livelock shape of round 3's hang (DESIGN.md
+// section 5b, "walker hang").
+__device__ __forceinline__ bool lead_lane() {
+    const unsigned long long ex = __ballot(1);
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(ex >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ex, 0u)) == 0u;
 }
 
 // A row descriptor read through the scalar cache: the row list is written by
@@ -726,7 +745,7 @@ __device__ __forceinline__ void fused_walk(const CascadeArgs &a, const WalkArgs 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
-    if (lane == 0) __hip_atomic_fetch_add(&w.int_ctl[1 + f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lead_lane()) __hip_atomic_fetch_add(&w.int_ctl[1 + f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Lazy grid (the default detect path).  The reference evaluates only the
@@ -823,7 +842,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         __builtin_amdgcn_s_setprio(SC_WALK_PRIO);  // latency-bound: issue ahead of the gathers
         for (;;) {
             int t = 0;
-            if (lane_id<RM>() == 0) t = atomicAdd(&w.int_ctl[0], 1);
+            if (lead_lane()) t = atomicAdd(&w.int_ctl[0], 1);
             t = __builtin_amdgcn_readfirstlane(t);
             if (t >= w.int_walks) break;
 #ifndef SC_NO_WALK
@@ -841,7 +860,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         const int c0 = c;
         while (c < a.n_frames) {
             int v = 0;
-            if (lane_id<RM>() == 0)
+            if (lead_lane())
                 v = __hip_atomic_load(&w.int_ctl[1 + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (__builtin_amdgcn_readfirstlane(v) < w.walks_per_frame) break;
             c++;
@@ -849,7 +868,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         if (c > c0) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane_id<RM>() == 0) __hip_atomic_fetch_max(cu_rdy, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lead_lane()) __hip_atomic_fetch_max(cu_rdy, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         return fr < c;
     };
@@ -858,6 +877,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     int st[kSlots], tq[kSlots], tt[kSlots], r[kSlots], j0[kSlots], nseg[kSlots];
     int frame[kSlots], level[kSlots], ys[kSlots];
     unsigned vtot = 0;  // windows this wave's chains visited (summed into row_visited at the end)
+    unsigned nspec = 0;  // speculative rounds this wave ran (summed into *w.spec at the end)
 #pragma unroll
     for (int sl = 0; sl < kSlots; sl++) st[sl] = 0;  // 0 empty, 1 waiting for entry, 2 active, 3 waiting for the frame's table
 
@@ -879,7 +899,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             pre--;
             const int q0 = q & ((1 << sh) - 1);  // an XCD of segment 0
             int v = 0;
-            if (lane_id<RM>() == 0) v = atomicAdd(&a.queues[(q0 * kSubQ + u) * kQueueStride], 1);
+            if (lead_lane()) v = atomicAdd(&a.queues[(q0 * kSubQ + u) * kQueueStride], 1);
             v = ((__builtin_amdgcn_readfirstlane(v) * kSubQ + u) << sh) + q0;
             if (v < n_tasks) {
                 t = v;
@@ -891,7 +911,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         }
         while (!drained) {
             int v = 0;
-            if (lane_id<RM>() == 0) v = atomicAdd(&a.queues[(q * kSubQ + u) * kQueueStride], 1);
+            if (lead_lane()) v = atomicAdd(&a.queues[(q * kSubQ + u) * kQueueStride], 1);
             v = ((__builtin_amdgcn_readfirstlane(v) * kSubQ + u) << sh) + (q & ((1 << sh) - 1));
             if (v < n_tasks) {
                 t = v;
@@ -914,7 +934,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
 #if SC_PROF_CHAIN  // task trace (profiling builds): realtime stamps per task at dequeue / start / finish
     auto stamp = [&](int sl, int which) {
         const long long ti = (long long)tt[sl] * nsg + tq[sl];
-        if (w.prof && lane_id<RM>() == 0 && ti < kTraceTasks)
+        if (w.prof && lead_lane() && ti < kTraceTasks)
             w.prof[16 + 2 * 8192 + 3 * ti + which] = __builtin_amdgcn_s_memrealtime();
     };
 #else
@@ -922,8 +942,12 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
 #endif
     auto finish = [&](int sl, int pos) {
         stamp(sl, 2);
-        if (lane_id<RM>() == 0) {
+        if (lead_lane()) {
+#if SC_TEST_HOOKS  // test builds only (a lost hand-off for the watchdog test): the check spills in the 16-wave kernel
+            if (tq[sl] + 1 < nsg && !(tq[sl] == 0 && tt[sl] + 1 == w.drop_task1))
+#else
             if (tq[sl] + 1 < nsg)
+#endif
                 __hip_atomic_store(&w.entry[(long long)tt[sl] * nsg + tq[sl] + 1], pos + 1,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -989,7 +1013,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
 #pragma unroll
             for (int sl = 0; sl < kSlots; sl++) {
                 e[sl] = 0;
-                if (st[sl] == 1 && lane_id<RM>() == 0)
+                if (st[sl] == 1 && lead_lane())
                     e[sl] = __hip_atomic_load(&w.entry[(long long)tt[sl] * nsg + tq[sl]], __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -1014,6 +1038,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                 if (spec < 0 && st[sl] == 1 && !((spd >> sl) & 1u)) spec = sl;
             if (spec >= 0) {
                 spd |= 1u << spec;
+                nspec++;
                 for (int i = lane_id<RM>(); i < 3 * nwords; i += 64) bits0[spec * 3 * nwords + i] = 0ull;
             }
         }
@@ -1025,18 +1050,25 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             }
             __builtin_amdgcn_s_sleep(4);
             // a lost hand-off must not hang the GPU: after 0.5 s of waiting (the
-            // chip-wide 100 MHz clock), or once any wave's watchdog has fired,
-            // the waiting tasks start anyway and the error word says so
+            // chip-wide 100 MHz clock) the waiting tasks start anyway, each
+            // counted in the sticky error word; once any wave's watchdog has
+            // fired in this launch (the per-launch flag), tasks waiting for
+            // an entry start at once (uncounted: the call raises already),
+            // while tasks waiting for their frame's table keep polling it
+            // (the walks always finish) unless their own wait timed out
             if (idle++ == 0) idle_t0 = __builtin_amdgcn_s_memrealtime();
             if ((idle & 255u) == 0u) {
                 int e = 0;
-                if (lane_id<RM>() == 0) e = __hip_atomic_load(w.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (__builtin_amdgcn_readfirstlane(e) != 0 ||
-                    __builtin_amdgcn_s_memrealtime() - idle_t0 > 50000000ull) {
+                if (lead_lane()) e = __hip_atomic_load(w.fired, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const bool own = __builtin_amdgcn_s_memrealtime() - idle_t0 > 50000000ull;
+                if (__builtin_amdgcn_readfirstlane(e) != 0 || own) {
 #pragma unroll
                     for (int sl = 0; sl < kSlots; sl++)
-                        if (st[sl] == 1 || st[sl] == 3) {
-                            if (lane_id<RM>() == 0) atomicAdd(w.err, 1);
+                        if (st[sl] == 1 || (own && st[sl] == 3)) {
+                            if (own && lead_lane()) {
+                                atomicAdd(w.err, 1);
+                                __hip_atomic_store(w.fired, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            }
                             start(sl, j0[sl]);
                         }
                     idle = 0;
@@ -1051,7 +1083,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
 #pragma unroll
         for (int i = 0; i < SC_ABL_EXTRA_RT; i++) {
             int v = 0;  // (word 1 of this XCD's queue line: unused, stays 0)
-            if (lane_id<RM>() == 0) v = atomicAdd(&a.queues[(q * kSubQ + u) * kQueueStride + 1], 0);
+            if (lead_lane()) v = atomicAdd(&a.queues[(q * kSubQ + u) * kQueueStride + 1], 0);
             v = __builtin_amdgcn_readfirstlane(v);
             if (v == 0x7fffffff) drained = true;
         }
@@ -1063,7 +1095,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
 #define SC_ACT(sl) (spec < 0 ? st[sl] == 2 : (sl) < 2)
 #pragma unroll
         for (int sl = 0; sl < kSlots; sl++) {
-            if (lane_id<RM>() == 0) {
+            if (lead_lane()) {
                 SlotDesc dd{};
                 if (SC_ACT(sl)) {
                     const int lv = SC_OF(level, sl), rr = spec < 0 ? r[sl] : sl, ns_ = SC_OF(nseg, sl);
@@ -1101,7 +1133,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             }
         // park the slot state in LDS across the evaluation: it would otherwise
         // stay live in SGPRs / VGPR lanes through the register-heavy item loop
-        if (lane_id<RM>() == 0) {
+        if (lead_lane()) {
 #pragma unroll
             for (int sl = 0; sl < kSlots; sl++) {
                 int *pk = park + sl * 10;
@@ -1173,7 +1205,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                         }
                     }
                     const unsigned long long gm = __ballot(good), dm = __ballot(det);
-                    if (lane_id<RM>() == 0) {
+                    if (lead_lane()) {
                         const int base = d + 128 * c;
                         or_spread(ev_, base, mk);
                         if (gm) or_spread(gd_, base, gm);
@@ -1222,7 +1254,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                 // lane (per-lane 64-bit LDS atomics on one or two words were
                 // the kernel's LDS bank conflicts)
                 const unsigned long long gm = __ballot(good), dm = __ballot(det);
-                if (lane_id<RM>() == 0) {
+                if (lead_lane()) {
                     const int base = r[sl] + 128 * c;
                     or_spread(ev_, base, mk);
                     if (gm) or_spread(gd_, base, gm);
@@ -1258,7 +1290,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                 } else if (qg < 64) {  // lands on good window qg, continues at qg + 1
                     vis = path & (qg == 63 ? ~0ull : ((2ull << qg) - 1ull));
                     const int k = (c << 6) + qg;
-                    if (lane_id<RM>() == 0 && ((dtw >> qg) & 1ull)) {  // detection (:203)
+                    if (lead_lane() && ((dtw >> qg) & 1ull)) {  // detection (:203)
                         const int slot = atomicAdd(&w.counters[0], 1);
                         atomicAdd(&w.counters[1 + w.frame0 + fr], 1);
                         if (slot < w.capacity) {
@@ -1294,19 +1326,20 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     // the visited count: only its sum is read (SC_INFO_VISITED), so one add
     // per wave instead of one returning-free atomic per task, spread over the
     // launch's words (the poll after a task's end waits for its atomics)
-    if (vtot && lane_id<RM>() == 0)
+    if (vtot && lead_lane())
         atomicAdd(&w.row_visited[(blockIdx.x * kChainWaves + wv) % (w.n_rows * a.n_frames)], vtot);
+    if (nspec && lead_lane()) atomicAdd(w.spec, (int)nspec);
 #undef SC_OF
 #undef SC_ACT
 #if SC_PROF_CHAIN
-    if (w.prof && lane_id<RM>() == 0) {  // this wave's start and exit times (launch timeline)
+    if (w.prof && lead_lane()) {  // this wave's start and exit times (launch timeline)
         const int gw = blockIdx.x * kChainWaves + wv;
         if (gw < 8192) {
             w.prof[16 + 2 * gw] = t_start;
             w.prof[17 + 2 * gw] = __builtin_amdgcn_s_memrealtime();
         }
     }
-    if (w.prof && lane_id<RM>() == 0) {
+    if (w.prof && lead_lane()) {
         atomicAdd(&w.prof[0], c_idle);
         atomicAdd(&w.prof[1], c_setup);
         atomicAdd(&w.prof[2], c_eval);
@@ -1356,7 +1389,7 @@ void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s) {
     hipLaunchKernelGGL(walk_kernel, dim3(a.n_rows * n_frames), dim3(64), 0, s, a);
 }
 
-int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hipStream_t s) {
+int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hipStream_t s, int *waves_out) {
     auto scratch = [&](int nw) { return nw * chain_wave_bytes(w.row_max) + w.n_levels * sizeof(LevelInfo) + 16; };
     const size_t kLds = 160 * 1024;
     // 16 waves with the weights in LDS when they fit and a frame's table sits
@@ -1389,6 +1422,7 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hi
     per_cu = std::max(1, std::min(per_cu, 4));
     if (c.wgs_per_cu > 0) per_cu = std::min(per_cu, c.wgs_per_cu);  // SC_OPT_WGS_PER_CU
     const int grid = std::max(1, c.cus) * per_cu;
+    if (waves_out) *waves_out = nw;
     if (nw == 16 && lw)
         hipLaunchKernelGGL((chain_kernel<true, 16>), dim3(grid), dim3(nt), lds, s, a, w);
     else if (nw == 16)

@@ -56,19 +56,24 @@ def _capacity(recs):
 def _frames_max(counts, group, b_max):
     """Frames per rank (len(counts) - 1) may differ between ranks (e.g. 257
     frames over 8 GPUs): the meta all_gather needs one size on every rank, so
-    without a caller-supplied b_max the ranks first all_gather their B."""
+    the ranks always all_gather their (B, b_max) first -- one tiny collective,
+    the same on every rank whether or not it passed b_max (a shortcut taken by
+    some ranks only would mismatch the collectives and hang).  A b_max below
+    some rank's B raises ValueError on EVERY rank (they all see the same
+    gathered values)."""
     import torch
     import torch.distributed as dist
     b = counts.numel() - 1
-    if b_max is not None:
-        if b > b_max:
-            raise ValueError("rank has %d frames, b_max %d" % (b, b_max))
-        return b_max
     world = dist.get_world_size(group)
-    mine = torch.tensor([b], dtype=torch.int64, device=counts.device)
-    bs = [torch.zeros_like(mine) for _ in range(world)]
-    dist.all_gather(bs, mine, group=group)
-    return int(max(int(x.item()) for x in bs))
+    mine = torch.tensor([b, -1 if b_max is None else int(b_max)], dtype=torch.int64, device=counts.device)
+    got = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(got, mine, group=group)
+    bs = [tuple(int(v) for v in x.tolist()) for x in got]
+    bm = max(x[0] for x in bs)
+    for r, (_b, m) in enumerate(bs):
+        if m >= 0 and m < bm:
+            raise ValueError("rank %d passed b_max %d but a rank has %d frames" % (r, m, bm))
+    return bm
 
 
 def _gather_meta(counts, recs, group, b_max=None):
@@ -109,8 +114,8 @@ def _gather_records(gm, counts, recs, group):
 def gather_detections(counts, recs, group=None, b_max=None):
     """counts: int32 [1+B] (counts[0] = this rank's total), recs: uint8
     [cap*40] record buffer (sc_enqueue_device's outputs).  B may differ
-    between ranks; b_max (the largest B, when the caller knows it) saves the
-    size exchange.
+    between ranks; b_max (optional, the largest B as a caller knows it) is
+    checked against the gathered sizes on every rank.
 
     1) all_gather of the counts (and capacities); 2) all_gather of every
     rank's first max(count) records (padded).  Raises RecordOverflow on every

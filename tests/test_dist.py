@@ -349,3 +349,44 @@ def test_gloo_stream_gather(cap):
         assert res[0] == "overflow" and res[2] > 3
     else:
         assert res[0] == "ok" and res[1] and res[2] > 0
+
+
+def _bmax_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from surfcascade_amd.dist import gather_detections
+    # rank 0: 3 frames and an advisory b_max that is too small for rank 1's
+    # 4 frames; rank 1 passes none.  Every rank must raise (no collective
+    # mismatch, no hang); then a consistent call still works.
+    B = 3 + rank
+    counts = torch.zeros(1 + B, dtype=torch.int32)
+    recs = torch.zeros(40 * 4, dtype=torch.uint8)
+    res = []
+    try:
+        gather_detections(counts, recs, b_max=3 if rank == 0 else None)
+        res.append("ok")
+    except ValueError as e:
+        res.append("raised" if "b_max" in str(e) else "other")
+    gc, _ = gather_detections(counts, recs, b_max=4 if rank == 1 else None)
+    res.append([len(c) for c in gc])
+    out_q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_b_max_mismatch_raises_on_every_rank():
+    """b_max passed by some ranks only must not desynchronise the
+    collectives; a b_max below another rank's frame count raises everywhere."""
+    import random
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29000 + random.randint(0, 900)
+    ps = [ctx.Process(target=_bmax_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        assert got[r] == ["raised", [4, 5]]

@@ -69,6 +69,116 @@ def test_c5_pedestrian_1080p_23_levels(sc, oracle, ped_cascade):
                  oracle.Params(base_len=64, aspect_h=2, n_levels=23))
 
 
+def _batch_parity(sc, oracle, cascade, model, frames, params_sc, params_or, **opts):
+    """One detect_batch call: every frame's table, evaluated windows, visited
+    set and detections against the oracle; returns the detector."""
+    det = sc.Detector(model, params_sc).set_options(**opts)
+    det.set_debug(True)
+    batch = det.detect_batch(frames, capacity=1 << 20)
+    H, W = frames.shape[1:]
+    layout, _ = oracle.grid_layout(W, H, params_or)
+    nvis_all = 0
+    for k in range(len(frames)):
+        T = oracle.integral(frames[k])
+        assert det.dump_integral(W, H, frame=k).view(np.uint32).tobytes() == T.view(np.uint32).tobytes()
+        p, s, v = det.dump_grid(frame=k)
+        rp, rs = oracle.eval_grid(T, cascade, params_or)
+        ev = p != -2
+        np.testing.assert_array_equal(p[ev], rp[ev])
+        assert s[ev].view(np.uint32).tobytes() == rs[ev].view(np.uint32).tobytes()
+        rv, _ = oracle.walk_grid(rp, rs, layout, cascade.n_stages, params_or.stride_score)
+        np.testing.assert_array_equal(v, rv)
+        ref, nvis = oracle.detect(T, cascade, params_or)
+        assert nvis == int(rv.sum())
+        assert _det_set(batch[k]) == _det_set(ref)
+        nvis_all += nvis
+    assert det.info("visited") == nvis_all
+    return det, batch
+
+
+def test_c5_bench_form_fused_12_waves(sc, oracle, ped_cascade):
+    """C5 exactly as bench.py runs it, in small: a batch of pedestrian 1080p
+    frames x 23 levels in one call, so the integral's column walks of frames
+    2.. run inside the 12-wave chain kernel (the fused walker + frame_ready
+    path of the pedestrian model's LDS-bound kernel; VERDICT r3 weak #1)."""
+    frames = np.stack([_frame(1920, 1080, 5100 + k) for k in range(4)])
+    params = sc.ScanParams.pedestrian(n_levels=23)
+    det, batch = _batch_parity(sc, oracle, ped_cascade, PED_CFG, frames, params,
+                               oracle.Params(base_len=64, aspect_h=2, n_levels=23))
+    assert det.info("fused_frames") == 2  # frames 2, 3: walks inside the chain kernel
+    assert det.info("chain_waves") == 12
+    assert det.info("column_pass") == 1   # frames 0, 1: rowcarry R rows + colsum
+
+
+def test_c4_bench_form_colstrip_one_launch(sc, oracle, face_cascade):
+    """C4 as bench.py runs it, in small: several 4K frames x 32 levels in ONE
+    chain launch (12 waves, tables beyond the Infinity Cache, no fusion)
+    whose tables colstrip built (VERDICT r3 weak #1).  Lowered thetas so every
+    level reaches detections."""
+    from surfcascade_amd import synth
+    c = face_cascade
+    text = synth.write_cfg(synth.cascade_tree(c.n_weak, np.full(c.n_stages, 0.45, np.float32),
+                                              c.patch_index, c.w, c.bias))
+    frames = np.stack([_frame(3840, 2160, 4100 + k) for k in range(3)])
+    det, batch = _batch_parity(sc, oracle, oracle.cascade_from_cfg(text), sc.Model.parse(text), frames,
+                               sc.ScanParams(n_levels=32), oracle.Params(n_levels=32), integral_passes=1)
+    assert det.info("column_pass") == 2  # colstrip
+    assert det.info("fused_frames") == 0
+    assert det.info("chain_waves") == 12
+    assert all(len(b) > 100 for b in batch)
+
+
+_WATCHDOG_CHILD = r"""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+import surfcascade_amd as sc
+from surfcascade_amd import synth
+host = np.stack([synth.make_frame(1280, 720, 700 + k) for k in range(2)])
+frames = torch.from_numpy(host).to("cuda:0")
+det = sc.Detector(sys.argv[2], sc.ScanParams(n_levels=6))
+recs = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda:0")
+counts = torch.zeros(3, dtype=torch.int32, device="cuda:0")
+det.enqueue_device(frames, recs, counts)
+det.synchronize()                              # clean
+det.set_option("test_drop_handoff", 5)
+det.enqueue_device(frames, recs, counts)       # step 1: one hand-off lost
+det.set_option("test_drop_handoff", -1)
+det.enqueue_device(frames, recs, counts)       # step 2: clean (rowcarry zeroes the per-call words)
+try:
+    det.synchronize()
+    print("NOT RAISED")
+except sc.SurfCascadeError as e:
+    print("RAISED", "hand-off" in str(e))
+det.enqueue_device(frames, recs, counts)
+det.synchronize()                              # reported once, not carried further
+print("CLEAN AFTER")
+"""
+
+
+def test_watchdog_error_is_sticky_over_pipelined_steps(sc):
+    """A lost segment hand-off (SC_OPT_TEST_DROP_HANDOFF, test-hook build
+    lib/testhooks) in the FIRST of two pipelined device steps is still raised
+    at the one synchronisation after the second (ADVICE r3: rowcarry used to
+    zero the watchdog word every call); the detector then works again.  The
+    product library refuses the hook."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=6))
+    with pytest.raises(sc.SurfCascadeError, match="test-hook build"):
+        det.set_option("test_drop_handoff", 5)
+    lib = os.path.join(ROOT, "surfcascade_amd", "lib", "testhooks", "libsurfcascade.so")
+    assert os.path.exists(lib), "test-hook library not built (__graft_entry__.build())"
+    env = dict(os.environ, SURFCASCADE_LIB=lib)
+    r = subprocess.run([sys.executable, "-c", _WATCHDOG_CHILD, ROOT, FACE_CFG], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "RAISED True" in r.stdout and "CLEAN AFTER" in r.stdout, r.stdout
+
+
 def test_c3_rank_shard_32_frames_one_call(sc, oracle, face_cascade):
     """The C3 per-rank workload: 32 device-resident 1080p frames in ONE
     sc_enqueue_device call (bench.py --gpus 8 shards 256 frames this way);

@@ -44,8 +44,10 @@ def test_integral_bit_exact(sc, oracle, W, H, seed, layout, passes):
     assert T.view(np.uint32).tobytes() == ref.view(np.uint32).tobytes()
 
 
-def _grid_parity(sc, oracle, cascade, cfg, img, params_sc, params_or, model_text=None, **opts):
+def _grid_parity(sc, oracle, cascade, cfg, img, params_sc, params_or, model_text=None, det_out=None, **opts):
     det = sc.Detector(sc.Model.parse(model_text) if model_text else cfg, params_sc).set_options(**opts)
+    if det_out is not None:
+        det_out.append(det)
     det.set_debug(True)
     wins = det.detect(img)
     p, s, v = det.dump_grid()
@@ -233,6 +235,23 @@ def test_chain_segments_per_row(sc, oracle, face_cascade, segs):
     img = _frame(1280, 720, 79)
     _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=8),
                  oracle.Params(n_levels=8), chain_segs=int(segs))
+
+
+@pytest.mark.parametrize("segs", [None, "8"])
+def test_speculative_rounds_run_and_match(sc, oracle, face_cascade, segs):
+    """One-frame launches (12 waves) speculate: an idle wave evaluates a
+    waiting task's first windows, both parities, before its entry arrives;
+    the task then enters mid-batch (rel > 0) over bits it did not clear.
+    The test asserts the path actually ran (SC_INFO_SPEC_ROUNDS) and that the
+    evaluated windows, visited set and detections are still the oracle's
+    (ADVICE r3), with the default 4 and with 8 segments per row (more
+    hand-offs, more waiting tasks, entries across segment boundaries)."""
+    img = _frame(1920, 1080, 1000)
+    dets = []
+    _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=24),
+                 oracle.Params(n_levels=24), det_out=dets, **({"chain_segs": int(segs)} if segs else {}))
+    assert dets[0].info("chain_waves") == 12
+    assert dets[0].info("spec_rounds") > 0
 
 
 @pytest.mark.parametrize("lds_weights", [None, "0"])
