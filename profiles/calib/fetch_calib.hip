@@ -20,6 +20,14 @@
 //                 stream: its L2 misses are Infinity-Cache hits -> the
 //                 gather ceiling of this shape
 //   k_mall_dense8 the k_dense8 shape over the 64 MiB table, 32 passes
+//   k_rows_<T>    (round 4) MI355X_MICROARCH.md's best gather form: whole
+//                 1-KiB pieces (64 lanes x 16 B, the chain kernel's dense
+//                 batch load) of random rows, staged through LDS
+//                 (global_load_dwordx4 + ds_write_b128, the guide's
+//                 register-staging form), one 4-wave workgroup per CU, 16
+//                 pieces per wave in flight (64 KiB per CU); tables of
+//                 64 MiB / 265 MiB (one C4 table) / 1 GiB: the beyond-L2
+//                 ceiling the chain kernel's fabric_frac is reported against
 // Each kernel: 256 CUs x 16 waves, every lane keeps 8 independent loads in
 // flight; a sum of the loaded words goes to `sink` so nothing is dead.
 //
@@ -29,6 +37,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 #define CHK(x)                                                                         \
@@ -109,6 +118,31 @@ __global__ __launch_bounds__(kThreads) void k_mall_dense8(const float4 *p, unsig
     if (a == 1234.5f) sink[0] = a;
 }
 
+// Random 1-KiB pieces staged through LDS: each wave loads kPieces pieces
+// (lane l: 16 B at piece + 16 l), writes them to its LDS tile, repeats
+// `steps` times; the rows (pieces) are a permutation of the table's pieces.
+constexpr int kPieces = 16;
+__global__ __launch_bounds__(256) void k_rows(const float4 *__restrict__ p, unsigned pieces, int steps,
+                                              float *sink) {
+    __shared__ float4 tile[4][kPieces][64];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const unsigned W = gridDim.x * 4, gw = blockIdx.x * 4 + wv;
+    float acc = 0.0f;
+    for (int st = 0; st < steps; st++) {
+        float4 v[kPieces];
+#pragma unroll
+        for (int u = 0; u < kPieces; u++) {
+            const unsigned g = (unsigned)st * W * kPieces + gw * kPieces + u;
+            const unsigned piece = (g * kMul) & (pieces - 1);
+            v[u] = p[(size_t)piece * 64 + lane];
+        }
+#pragma unroll
+        for (int u = 0; u < kPieces; u++) tile[wv][u][lane] = v[u];
+        acc += tile[wv][(lane + st) & (kPieces - 1)][lane ^ 1].x;
+    }
+    if (acc == 1234.5f) sink[0] = acc;
+}
+
 __global__ void k_fill(float4 *p, size_t n4, unsigned seed) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
         const unsigned h = (unsigned)i * 2654435761u ^ seed;
@@ -179,6 +213,26 @@ int main() {
     timed("k_mall_dense8",
           [&] { hipLaunchKernelGGL(k_mall_dense8, dim3(grid), dim3(kThreads), 0, 0, ps, small_lines, sink, passes); },
           128.0 * small_lines * passes, (size_t)small_lines * passes, 4);
+    // round 4: 1-KiB row pieces through LDS (the guide's gather-into-LDS
+    // form) from 64 MiB, 265 MiB and 1 GiB tables; each table warmed by one
+    // untimed launch, then timed launches of the same permutation order
+    for (size_t tb : {64ull << 20, 256ull << 20, 1ull << 30}) {
+        float4 *pt = tb == big ? pb : nullptr;
+        if (!pt) {
+            CHK(hipMalloc(&pt, tb));
+            hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, pt, tb / 16, 4u);
+        }
+        const unsigned pcs = (unsigned)(tb / 1024);
+        const int steps = (int)std::max<size_t>(1, (size_t)pcs * 4 / ((size_t)cus * 4 * kPieces));  // ~4 table passes
+        auto go = [&] { hipLaunchKernelGGL(k_rows, dim3(cus), dim3(256), 0, 0, pt, pcs, steps, sink); };
+        go();
+        CHK(hipDeviceSynchronize());
+        const size_t n_lines = (size_t)cus * 4 * kPieces * steps * 8;
+        char name[64];
+        std::snprintf(name, sizeof name, "k_rows_%zuMiB", tb >> 20);
+        timed(name, go, 128.0 * n_lines, n_lines, 4);
+        if (pt != pb) CHK(hipFree(pt));
+    }
     CHK(hipFree(pb));
     CHK(hipFree(ps));
     CHK(hipFree(pf));

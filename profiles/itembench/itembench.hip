@@ -732,6 +732,69 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_fold(Args a) {
     }
 }
 
+// V14 (round 4 ablation, wrong results, timing only): the LDS-path ceiling of
+// the item loop.  Every corner is read from a 64 KiB table tile in the
+// workgroup's LDS (ds_read_b128 at the global cell offset mod 4096, so the
+// lanes of a wave instruction keep the production access pattern: consecutive
+// windows -> consecutive 16-B cells, same bank spread) instead of through
+// the texture path; the tile is staged once per workgroup (no staging cost
+// in the loop).  Same corner slots, box sums, Normalize, LR, sigmoid: the
+// time an item loop would take if every gather were an LDS hit for free.
+constexpr int kTileCells = 4096;  // 64 KiB of float4
+template <class P>
+__device__ __forceinline__ void features_lds(const float4 *tile, unsigned org, int half_off, const P &pj,
+                                             f2 (&fp)[16]) {
+    int off[10];
+    corner_offsets(pj, off);
+    f2 h[2][8];
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++) {
+        float4 cn[10];
+#pragma unroll
+        for (int m = 0; m < 10; m++) cn[m] = tile[(org + (unsigned)(hh * half_off + off[m])) & (kTileCells - 1)];
+        half_box(pj.shape, cn, h[hh]);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        fp[4 * c] = h[0][2 * c];
+        fp[4 * c + 1] = h[0][2 * c + 1];
+        fp[4 * c + 2] = h[1][2 * c];
+        fp[4 * c + 3] = h[1][2 * c + 1];
+    }
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_ldsgather(Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4 *Wl; double *Bl; int4 *Rl; float *Sc;
+    stage<WAVES>(a, smem, Wl, Bl, Rl, Sc);
+    float4 *tile = reinterpret_cast<float4 *>(smem + (((size_t)a.K * (144 + 8 + 16) + a.n_levels * 4 + 63) & ~(size_t)63));
+    for (int i = threadIdx.x; i < kTileCells; i += WAVES * 64) tile[i] = a.table[(size_t)a.g.rowp * 400 + i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const unsigned q0 = xcc();
+    for (unsigned qi = 0; qi < 8; qi++) {
+      const unsigned q = (q0 + qi) & 7;
+      const Item *I = a.items + q * a.cap;
+      float *O = a.out + q * a.cap;
+      const int n = a.n_items[q];
+      for (;;) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&a.tickets[q * 64], 1);
+        b0 = __builtin_amdgcn_readfirstlane(b0) * kChunk * kBlock;
+        if (b0 >= n) break;
+        const int b1 = min(n, b0 + kChunk * kBlock);
+        for (int i = b0 + lane; i < b1; i += 64) {
+            const Item it = I[i];
+            f2 fp[16];
+            features_lds(tile, it.origin, a.g.hs, project(a, Rl, Sc, it), fp);
+            normalize2(fp);
+            O[i] = lr_predict2(fp, Wl + it.k * 9, Bl[it.k]);
+        }
+      }
+    }
+}
+
 }  // namespace
 
 extern "C" int ib_run(int variant, int waves, const Args *a, void *stream) {
@@ -770,6 +833,11 @@ extern "C" int ib_run(int variant, int waves, const Args *a, void *stream) {
     } else if (variant == 13) {
         if (waves == 12) hipLaunchKernelGGL((k_xswap<12, 16>), dim3(cus), dim3(768), lds, s, *a);
         else if (waves == 16) hipLaunchKernelGGL((k_xswap<16, 16>), dim3(cus), dim3(1024), lds, s, *a);
+        else return -1;
+    } else if (variant == 14) {  // LDS-path ceiling: + the 64 KiB tile
+        const size_t lt = ((lds + 63) & ~(size_t)63) + kTileCells * 16;
+        if (waves == 12) hipLaunchKernelGGL((k_ldsgather<12>), dim3(cus), dim3(768), lt, s, *a);
+        else if (waves == 16) hipLaunchKernelGGL((k_ldsgather<16>), dim3(cus), dim3(1024), lt, s, *a);
         else return -1;
     } else if (variant == 3) {
         if (waves == 8) L(k_fold, 8); else if (waves == 12) L(k_fold, 12); else if (waves == 16) L(k_fold, 16); else return -1;
