@@ -36,6 +36,24 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 # VALU issue ceiling: 256 CUs x 4 SIMDs, a wave64 VALU instruction every 2
 # cycles per SIMD (SIMD-32), 2.4 GHz (MI355X_MICROARCH.md: wave scheduling)
 VALU_ISSUE_PEAK = 1024 * 0.5 * 2.4e9
+# the texture data path (TD): one per CU, 64 B/clk, so a 16-B-per-lane wave
+# load returns its 1 KiB in 16 cycles whatever its active lanes (DESIGN.md
+# 5a, calibrated against TD_TD_BUSY)
+TD_CYCLES_PER_LOAD = 16
+N_CUS = 256
+# the sources whose compiled code the PMC table (profiles/pmc_windows.json)
+# describes: an entry collected on other sources is stale and not reported
+KERNEL_SOURCES = ("sc_windows.hip", "sc_device.hpp", "sc_kernels.hpp", "sc_integral_dev.hpp", "sc_integral.hip")
+
+
+def kernel_sources_sha():
+    """sha256 (16 hex) over the window / integral kernel sources."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, "surfcascade_amd", "csrc", f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
 
 
 MODELS = os.path.join(ROOT, "surfcascade_amd", "models")
@@ -458,6 +476,10 @@ def main():
         pipe_bytes = W * H + 64 * (W + 1) * (H + 1)
         pipe_s = max(sum(v[0] for v in kt.values()) / 1e3 / max(n_win, 1), 1e-12)
         pmc = pmc_for(args, B, W) if not opts and not stub else {}
+        src_sha = kernel_sources_sha()
+        pmc_stale = bool(pmc) and pmc.get("kernel_sources_sha") != src_sha
+        if pmc_stale:  # collected on other kernel sources: its counters describe another binary
+            pmc = {"source": pmc.get("source"), "stale": True}
         traffic, valu_insts = pmc.get("hbm_bytes_per_launch"), pmc.get("valu_insts_per_launch")
         line = {
             "metric": CONFIGS[args.config]["metric"],
@@ -485,6 +507,7 @@ def main():
             "roofline": roofline(achieved, traffic, valu_insts, avg_win_s, win_bytes, pipe_bytes * B,
                                  pipe_s, pmc, opts, fused),
             "kernel_ms_per_launch": {k: v[0] / max(v[1], 1) for k, v in kt.items()},
+            "kernel_sources_sha": src_sha,
             "visited_windows_last_step": visited,
             "detections_last_step": total_det,
         }
@@ -517,7 +540,8 @@ def main():
 def pmc_for(args, B, W):
     """PMC per launch of the window kernel for this workload (profiles/
     pmc_windows.json, keyed per config; written by profiles/pmc_summary.py from
-    the committed rocprofv3 passes), or {}."""
+    the committed rocprofv3 passes), or {}.  The table's measured ceilings
+    (top-level "ceilings") are merged into the entry."""
     pmc_path = os.path.join(ROOT, "profiles", "pmc_windows.json")
     if not os.path.exists(pmc_path):
         return {}
@@ -527,7 +551,7 @@ def pmc_for(args, B, W):
     for e in entries:
         if (e.get("batch") == B and e.get("width") == W and e.get("levels") == args.levels
                 and e.get("config", "C2") == args.config):
-            return e
+            return dict(e, **{k: v for k, v in pm.get("ceilings", {}).items() if k not in e})
     return {}
 
 
@@ -549,22 +573,38 @@ def roofline(achieved, traffic, valu_insts, avg_win_s, bytes_launch, pipe_bytes,
          "valu": (valu_insts / VALU_ISSUE_PEAK / avg_win_s) if valu_insts else None,
          "valu_insts_per_launch": valu_insts, "valu_peak_per_s": VALU_ISSUE_PEAK,
          "pmc_source": pmc.get("source")}
+    if pmc.get("stale"):
+        r["pmc_stale"] = ("profiles/pmc_windows.json was collected on other kernel sources "
+                          "(kernel_sources_sha differs): traffic, valu, fabric and TD fields omitted")
+        return r
+    c = pmc.get("counters_per_launch", {})
     # the level the kernel actually stresses: L2 misses (128-B lines from the
-    # Infinity Cache / HBM, TCC_MISS) per second over the measured gather
-    # ceiling of the same 16-B-per-lane shape (profiles/calib, k_mall_sparse)
-    miss = pmc.get("counters_per_launch", {}).get("TCC_MISS_sum")
+    # Infinity Cache / HBM, TCC_MISS) per second over the measured beyond-L2
+    # ceiling of 1-KiB row gathers through LDS (profiles/calib k_rows, the
+    # guide's best gather form) for a table that fits the Infinity Cache,
+    # and for C4's beyond-Infinity-Cache tables the same form's HBM figure
+    miss = c.get("TCC_MISS_sum")
     ceil = pmc.get("fabric_ceiling_lines_per_s")
     if miss and ceil:
         r["fabric_lines_per_s"] = miss / avg_win_s
         r["fabric_ceiling_lines_per_s"] = ceil
+        r["fabric_ceiling_source"] = pmc.get("fabric_ceiling_source")
         r["fabric_frac"] = miss / avg_win_s / ceil
-        hit = pmc["counters_per_launch"].get("TCC_HIT_sum")
+        hit = c.get("TCC_HIT_sum")
         r["l2_hit"] = hit / (hit + miss) if hit else None
-        # a table beyond the Infinity Cache (C4) gathers from HBM: the same
-        # shape's cold-HBM ceiling (profiles/calib k_sparse)
         hceil = pmc.get("hbm_gather_ceiling_lines_per_s")
         if hceil:
             r["hbm_gather_frac"] = miss / avg_win_s / hceil
+    # the texture data path: busy cycles (transfer + waits for data) and the
+    # transfer alone (16 cycles per load instruction) over the launch's cycles
+    # (GRBM_GUI_ACTIVE summed over the 8 XCDs), per CU
+    cyc = c.get("GRBM_GUI_ACTIVE")
+    if cyc and c.get("SQ_INSTS_VMEM_RD"):
+        cyc_xcd = cyc / 8.0
+        r["td_frac"] = c["SQ_INSTS_VMEM_RD"] * TD_CYCLES_PER_LOAD / (N_CUS * cyc_xcd)
+        if c.get("TD_TD_BUSY_sum"):
+            r["td_busy_frac"] = c["TD_TD_BUSY_sum"] / (N_CUS * cyc_xcd)
+        r["clock_ghz_from_grbm"] = cyc_xcd / (pmc.get("avg_launch_ms_pmc") or avg_win_s * 1e3) / 1e6
     return r
 
 

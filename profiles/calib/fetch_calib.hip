@@ -25,8 +25,10 @@
 //                 batch load) of random rows, staged through LDS
 //                 (global_load_dwordx4 + ds_write_b128, the guide's
 //                 register-staging form), one 4-wave workgroup per CU, 16
-//                 pieces per wave in flight (64 KiB per CU); tables of
-//                 64 MiB / 265 MiB (one C4 table) / 1 GiB: the beyond-L2
+//                 pieces per wave in flight (64 KiB per CU); k_rows_dma_<T>
+//                 the same pieces by LDS DMA (global_load_lds_dwordx4);
+//                 tables of 32 / 64 / 256 MiB (~ one C4 table) / 1 GiB:
+//                 the beyond-L2
 //                 ceiling the chain kernel's fabric_frac is reported against
 // Each kernel: 256 CUs x 16 waves, every lane keeps 8 independent loads in
 // flight; a sum of the loaded words goes to `sink` so nothing is dead.
@@ -143,6 +145,29 @@ __global__ __launch_bounds__(256) void k_rows(const float4 *__restrict__ p, unsi
     if (acc == 1234.5f) sink[0] = acc;
 }
 
+// The same pieces by LDS DMA (global_load_lds_dwordx4: per-lane source,
+// the wave's 1 KiB lands contiguous in its LDS ring), nothing read back
+// until the end: as many pieces in flight as the vector-memory counter
+// allows (the guide's gather-into-LDS form without a consumer)
+__global__ __launch_bounds__(256) void k_rows_dma(const float4 *__restrict__ p, unsigned pieces, int steps,
+                                                  float *sink) {
+    __shared__ float4 ring[4][kPieces][64];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const unsigned W = gridDim.x * 4, gw = blockIdx.x * 4 + wv;
+    for (int st = 0; st < steps; st++) {
+#pragma unroll
+        for (int u = 0; u < kPieces; u++) {
+            const unsigned g = (unsigned)st * W * kPieces + gw * kPieces + u;
+            const unsigned piece = (g * kMul) & (pieces - 1);
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(p + (size_t)piece * 64 + lane),
+                (__attribute__((address_space(3))) void *)&ring[wv][u][0], 16, 0, 0);
+        }
+    }
+    __syncthreads();
+    if (ring[wv][lane & (kPieces - 1)][lane].x == 1234.5f) sink[0] = 1.0f;
+}
+
 __global__ void k_fill(float4 *p, size_t n4, unsigned seed) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
         const unsigned h = (unsigned)i * 2654435761u ^ seed;
@@ -216,7 +241,7 @@ int main() {
     // round 4: 1-KiB row pieces through LDS (the guide's gather-into-LDS
     // form) from 64 MiB, 265 MiB and 1 GiB tables; each table warmed by one
     // untimed launch, then timed launches of the same permutation order
-    for (size_t tb : {64ull << 20, 256ull << 20, 1ull << 30}) {
+    for (size_t tb : {32ull << 20, 64ull << 20, 256ull << 20, 1ull << 30}) {
         float4 *pt = tb == big ? pb : nullptr;
         if (!pt) {
             CHK(hipMalloc(&pt, tb));
@@ -224,13 +249,18 @@ int main() {
         }
         const unsigned pcs = (unsigned)(tb / 1024);
         const int steps = (int)std::max<size_t>(1, (size_t)pcs * 4 / ((size_t)cus * 4 * kPieces));  // ~4 table passes
-        auto go = [&] { hipLaunchKernelGGL(k_rows, dim3(cus), dim3(256), 0, 0, pt, pcs, steps, sink); };
-        go();
-        CHK(hipDeviceSynchronize());
         const size_t n_lines = (size_t)cus * 4 * kPieces * steps * 8;
-        char name[64];
-        std::snprintf(name, sizeof name, "k_rows_%zuMiB", tb >> 20);
-        timed(name, go, 128.0 * n_lines, n_lines, 4);
+        for (int dma = 0; dma < 2; dma++) {
+            auto go = [&] {
+                if (dma) hipLaunchKernelGGL(k_rows_dma, dim3(cus), dim3(256), 0, 0, pt, pcs, steps, sink);
+                else hipLaunchKernelGGL(k_rows, dim3(cus), dim3(256), 0, 0, pt, pcs, steps, sink);
+            };
+            go();
+            CHK(hipDeviceSynchronize());
+            char name[64];
+            std::snprintf(name, sizeof name, "k_rows%s_%zuMiB", dma ? "_dma" : "", tb >> 20);
+            timed(name, go, 128.0 * n_lines, n_lines, 4);
+        }
         if (pt != pb) CHK(hipFree(pt));
     }
     CHK(hipFree(pb));
