@@ -579,10 +579,9 @@ def roofline(achieved, traffic, valu_insts, avg_win_s, bytes_launch, pipe_bytes,
         return r
     c = pmc.get("counters_per_launch", {})
     # the level the kernel actually stresses: L2 misses (128-B lines from the
-    # Infinity Cache / HBM, TCC_MISS) per second over the measured beyond-L2
-    # ceiling of 1-KiB row gathers through LDS (profiles/calib k_rows, the
-    # guide's best gather form) for a table that fits the Infinity Cache,
-    # and for C4's beyond-Infinity-Cache tables the same form's HBM figure
+    # Infinity Cache / HBM, TCC_MISS) per second over the beyond-L2 gather
+    # ceiling: the guide's best gather into LDS (8.6 TB/s) or the best our
+    # calibration kernels measured, whichever is higher (profiles/calib)
     miss = c.get("TCC_MISS_sum")
     ceil = pmc.get("fabric_ceiling_lines_per_s")
     if miss and ceil:
@@ -592,9 +591,8 @@ def roofline(achieved, traffic, valu_insts, avg_win_s, bytes_launch, pipe_bytes,
         r["fabric_frac"] = miss / avg_win_s / ceil
         hit = c.get("TCC_HIT_sum")
         r["l2_hit"] = hit / (hit + miss) if hit else None
-        hceil = pmc.get("hbm_gather_ceiling_lines_per_s")
-        if hceil:
-            r["hbm_gather_frac"] = miss / avg_win_s / hceil
+        if pmc.get("fabric_ceiling_measured_lines_per_s"):
+            r["fabric_ceiling_measured_lines_per_s"] = pmc["fabric_ceiling_measured_lines_per_s"]
     # the texture data path: busy cycles (transfer + waits for data) and the
     # transfer alone (16 cycles per load instruction) over the launch's cycles
     # (GRBM_GUI_ACTIVE summed over the 8 XCDs), per CU

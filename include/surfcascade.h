@@ -195,14 +195,13 @@ int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, 
                                 /* launch (12 or 16; 0: none yet)              */
 #define SC_INFO_COLUMN_PASS 8   /* the last call's integral column pass for the */
                                 /* frames built outside the chain kernel:      */
-                                /* 1 two-pass (rowcarry R + colsum), 2 colstrip, */
-                                /* 3 both passes in one launch (one frame)     */
+                                /* 1 two-pass (rowcarry R + colsum), 2 colstrip */
 #define SC_INFO_SPEC_ROUNDS 9   /* speculative evaluation rounds of the last    */
                                 /* chain launch (one-frame launches only)      */
 int sc_detector_info(sc_detector *d, int what, int64_t *value);
 
 /* ---- tuning and test options ---------------------------------------------
- * Options 1-14, 17-19 and 21 are schedule / layout choices that never change a result bit
+ * Options 1-14 and 17-19 are schedule / layout choices that never change a result bit
  * (tests/test_gpu_parity.py runs each against the oracle); the defaults are
  * the measured-fastest.  Options 15-16 restrict the scan to a range of levels
  * (profiling of level groups): they DO change the result, to the windows of
@@ -243,9 +242,6 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
                               /* launch has 2+ frames                          */
 #define SC_OPT_INTEGRAL_PRE 19 /* fused: frames per launch integrated before   */
                               /* the chain kernel (0: default 2)               */
-#define SC_OPT_INTEGRAL_ONE 21 /* one-frame calls: the integral's rowcarry and */
-                              /* colsum passes in one launch (0 auto, 1 two   */
-                              /* launches)                                    */
 #define SC_OPT_TEST_DROP_HANDOFF 20 /* test only (-1 off): the chain kernel drops */
                               /* the segment-0 hand-off of row task `value`  */
                               /* of every launch; the watchdog must then     */

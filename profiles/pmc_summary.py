@@ -57,29 +57,63 @@ def sources_sha(d):
     return shas.pop()
 
 
-def ceilings(calib):
-    """Beyond-L2 gather ceilings from profiles/calib fetch_calib's k_rows_<T>MiB
-    lines (1-KiB row pieces through LDS, MI355X_MICROARCH.md's best gather
-    form): requested lines/s x (1 - 4 MiB / T), the share of a uniformly
-    gathered table an XCD's L2 holds; the fabric ceiling is the best table
-    that fits the Infinity Cache, the HBM one the 1 GiB table."""
-    fab, hbm = None, None
+# MI355X_MICROARCH.md (section "Indexed rows: gather into LDS"): 1,152-B rows
+# gathered into LDS from a 38 MB Infinity-Cache-resident table, 8.6 TB/s --
+# the best gather rate the guide measured beyond the L2
+GUIDE_GATHER_LDS_BPS = 8.6e12
+
+
+def ceilings(calib, calib_pmc=None):
+    """Beyond-L2 gather ceilings (lines/s).  Measured: profiles/calib
+    fetch_calib's gather kernels (k_rows*, k_mall_*: 1-KiB row pieces through
+    LDS, 16-B-per-lane gathers), requested lines/s x (1 - L2 hit rate) -- the
+    hit rate from the calibration run's TCC_HIT / TCC_MISS (calib_pmc) when
+    given, else 4 MiB / T for a T-MiB table.  The fabric ceiling is the
+    larger of the best measured rate (tables <= 256 MiB) and the guide's 8.6
+    TB/s; nothing the chain kernel reaches may exceed it (it did exceed the
+    round-3 same-shape figure at C4)."""
+    import collections
+    hit = {}
+    if calib_pmc:
+        per = collections.defaultdict(lambda: collections.defaultdict(float))
+        for row in csv.DictReader(open(calib_pmc)):
+            per[(row["Kernel_Name"].split("(")[0].strip(), row["Dispatch_Id"])][row["Counter_Name"]] += \
+                float(row["Counter_Value"])
+        by_kernel = collections.defaultdict(list)
+        for (name, did), c in sorted(per.items(), key=lambda kv: int(kv[0][1])):
+            if c.get("TCC_HIT_sum", 0) + c.get("TCC_MISS_sum", 0) > 0:
+                by_kernel[name].append(c["TCC_HIT_sum"] / (c["TCC_HIT_sum"] + c["TCC_MISS_sum"]))
+        # k_mall_*: one table (64 MiB); k_rows / k_rows_dma: one warm + 4 timed
+        # dispatches per table size, in fetch_calib's order
+        for name, v in by_kernel.items():
+            if name.startswith("k_rows"):
+                for i, t in enumerate((32, 64, 256, 1024)):
+                    if len(v) >= 5 * (i + 1):
+                        hit["%s_%dMiB" % (name, t)] = min(v[5 * i:5 * i + 5])
+            else:
+                hit[name] = min(v)
+    best, best_k, hbm = 0.0, None, None
     for line in open(calib):
         if not line.startswith("{"):
             continue
         d = json.loads(line)
-        if not d["kernel"].startswith("k_rows_"):
+        k = d["kernel"]
+        m = re.search(r"(\d+)MiB$", k)
+        t_mib = int(m.group(1)) if m else (64 if k.startswith("k_mall") else None)
+        if t_mib is None:
             continue
-        t_mib = int(re.search(r"(\d+)MiB$", d["kernel"]).group(1))
-        beyond = d["lines_per_s"] * (1.0 - 4.0 / t_mib)
-        if t_mib <= 256:
-            fab = max(fab or 0.0, beyond)
-        else:
-            hbm = beyond
-    return {"fabric_ceiling_lines_per_s": fab, "hbm_gather_ceiling_lines_per_s": hbm,
-            "fabric_ceiling_source": "profiles/calib k_rows_<T>MiB (%s): 1-KiB random row pieces staged "
-                                     "through LDS, requested lines/s x (1 - 4 MiB/T); fabric = best T <= "
-                                     "256 MiB, HBM = 1 GiB" % calib}
+        h = hit.get(k, 4.0 / t_mib)
+        beyond = d["lines_per_s"] * (1.0 - h)
+        if t_mib <= 256 and beyond > best:
+            best, best_k = beyond, k
+        if t_mib > 256 and k.startswith("k_rows"):
+            hbm = max(hbm or 0.0, beyond)
+    guide = GUIDE_GATHER_LDS_BPS / 128.0
+    return {"fabric_ceiling_lines_per_s": max(best, guide), "fabric_ceiling_measured_lines_per_s": best,
+            "hbm_gather_ceiling_lines_per_s": hbm,
+            "fabric_ceiling_source": "max(MI355X_MICROARCH.md gather-into-LDS 8.6 TB/s = %.3g lines/s, best "
+                                     "measured beyond-L2 gather %.3g lines/s (%s, %s))"
+                                     % (guide, best, best_k, calib)}
 
 
 def main():
@@ -93,6 +127,7 @@ def main():
     ap.add_argument("--levels", type=int, default=24)
     ap.add_argument("--calib", help="profiles/calib fetch_calib output (k_rows_* lines): the beyond-L2 "
                                     "gather ceilings for fabric_frac (stored top-level in the JSON)")
+    ap.add_argument("--calib-pmc", help="the calibration run's pmc_counter_collection.csv (TCC hit rates)")
     a = ap.parse_args()
     res = load(a.dir)
     for k, cs in sorted(res.items()):
@@ -121,7 +156,7 @@ def main():
             if "configs" not in doc:
                 doc = {"configs": {doc.get("config", "C2"): doc}}
         if a.calib:
-            doc["ceilings"] = ceilings(a.calib)
+            doc["ceilings"] = ceilings(a.calib, a.calib_pmc)
         doc.setdefault("configs", {})[a.config] = out
         json.dump(doc, open(a.json, "w"), indent=1)
 

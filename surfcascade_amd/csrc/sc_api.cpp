@@ -132,7 +132,6 @@ struct sc_detector {
         int integral_fuse = 0;           // column walks inside the chain kernel: 0 auto, 1 never, 2 from 2 frames
         int integral_pre = 0;            // fused: frames integrated before the chain kernel (0: 2)
         int drop_handoff = -1;           // test only: task whose segment-0 hand-off is dropped (watchdog)
-        int integral_one = 0;            // one frame: the integral's two passes in one launch (0 auto, 1 never)
     } opt;
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
@@ -168,9 +167,7 @@ struct sc_detector {
     // touch it, so a timeout in any pipelined step is still raised at the
     // next synchronisation); zeroed once at allocation and after each read
     DevBuf<int> d_err;
-    bool err_armed = false;       // a launch since the last check_chain that may count into d_err
-    DevBuf<int> d_rowflag;        // one-frame integral: per-row publication tags (integral1_kernel)
-    int row_epoch = 0;            // ... the tag of the last call
+    bool chain_launched = false;  // a chain launch since the last check_chain
     DevBuf<int8_t> d_st_p;      // per grid window: stage reached (-1 prefilter reject)
     DevBuf<float> d_st_s;       // per grid window: last stage score
     // debug
@@ -206,7 +203,7 @@ struct sc_detector {
         d_proj_all.release(); d_mine_cnt.release(); d_mine_off.release(); d_mine_win.release();
         d_feat.release();
         d_frames.release(); d_table.release(); d_carry.release(); d_out.release(); d_counters.release();
-        d_visited.release(); d_queues.release(); d_entry.release(); d_err.release(); d_rowflag.release(); d_st_p.release(); d_st_s.release();
+        d_visited.release(); d_queues.release(); d_entry.release(); d_err.release(); d_st_p.release(); d_st_s.release();
         d_dbg_v.release(); d_prof.release();
         h_stage.release();
         if (stream) (void)hipStreamDestroy(stream);
@@ -697,27 +694,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     ra.rfull_n = fuse ? (two_pass_pre ? std::min(pre, n) : 0) : (two_pass_all ? n : 0);
     hipEvent_t e0 = nullptr;
     timed_begin(d, &e0);
-    // one frame, two-pass: rowcarry4's rows and colsum4's walks in ONE launch,
-    // the walks following the rows down (SC_OPT_INTEGRAL_ONE; bit-identical)
-    bool one = false;
-    if (n == 1 && !fuse && two_pass_all && ra.rfull_n >= 1 && d->opt.integral_one != 1) {
-        if (d->d_rowflag.n < (size_t)H) {
-            d->d_rowflag.ensure((size_t)H);
-            HIPCHK(hipMemsetAsync(d->d_rowflag.p, 0, sizeof(int) * (size_t)H, d->stream));
-            d->row_epoch = 0;
-        }
-        if (!d->d_err.p) {
-            d->d_err.ensure(1);
-            HIPCHK(hipMemsetAsync(d->d_err.p, 0, sizeof(int), d->stream));
-        }
-        if (++d->row_epoch <= 0) {  // (2^31 calls: start the tags again from a cleared array)
-            HIPCHK(hipMemsetAsync(d->d_rowflag.p, 0, sizeof(int) * d->d_rowflag.n, d->stream));
-            d->row_epoch = 1;
-        }
-        one = sc::launch_integral1(ra, d->row_epoch, d->d_rowflag.p, d->d_err.p, d->stream);
-        if (one) d->err_armed = true;
-    }
-    const bool have_r = one || sc::launch_rowscan(ra, n, d->stream);
+    const bool have_r = sc::launch_rowscan(ra, n, d->stream);
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_ROWSCAN, e0);
 
@@ -726,11 +703,9 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     // row-parallel two-pass form is shorter (SC_OPT_INTEGRAL_PASSES overrides)
     const long long carry_frame = (long long)H * ((W + sc::kStrip - 1) / sc::kStrip) * 8;  // u32 per frame
 #if defined(SC_WALK_STORE) && SC_WALK_STORE == 0  // timing ablation: walks store nothing, tables built here
-    if (one) {
-    } else if (false) {
+    if (false) {
 #else
-    if (one) {  // (the column pass ran inside integral1)
-    } else if (fuse) {  // only the first `pre` frames of each launch here
+    if (fuse) {  // only the first `pre` frames of each launch here
 #endif
         for (int f0 = 0; f0 < n; f0 += chunk) {
             sc::RowScanArgs rc = ra;
@@ -742,7 +717,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     } else {
         sc::launch_colscan(ra, n, two_pass_all, d->stream, have_r);
     }
-    d->last_colpass = one ? 3 : (fuse ? two_pass_pre : two_pass_all) ? 1 : 2;
+    d->last_colpass = (fuse ? two_pass_pre : two_pass_all) ? 1 : 2;
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_COLSCAN, e0);
 
@@ -822,7 +797,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             wc.int_ctl = wc.fired + 1;
             wc.spec = wc.int_ctl + 1 + std::min(chunk, n);
             d->spec_word = wc.spec - d->d_entry.p;
-            d->err_armed = true;
+            d->chain_launched = true;
             if (fuse && nc > pre) {
                 wc.frames = d_frames + (long long)f0 * H * stride;
                 wc.frame_bytes = (long long)H * stride;
@@ -867,14 +842,13 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
 // The chain kernel's hand-off watchdog (reads after the stream has drained):
 // every launch since the last check, pipelined steps included.
 void check_chain(sc_detector *d) {
-    if (!d->err_armed || !d->d_err.p) return;
-    d->err_armed = false;
+    if (!d->lazy || !d->chain_launched || !d->d_err.p) return;
+    d->chain_launched = false;
     int err = 0;
     HIPCHK(hipMemcpy(&err, d->d_err.p, sizeof(int), hipMemcpyDeviceToHost));
     if (err) {
         HIPCHK(hipMemset(d->d_err.p, 0, sizeof(int)));
-        throw Error{SC_ERR_DEVICE, "chain kernel / one-frame integral: " + std::to_string(err) +
-                                       " segment hand-off(s) or integral row(s) timed out"};
+        throw Error{SC_ERR_DEVICE, "chain kernel: " + std::to_string(err) + " segment hand-off(s) timed out"};
     }
     if (d->d_prof.p) {
         unsigned long long pc[16];
@@ -1573,7 +1547,6 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
             case SC_OPT_INTEGRAL_PASSES: o.integral_passes = range(0, 2); regeo = false; break;
             case SC_OPT_INTEGRAL_FUSE: o.integral_fuse = range(0, 2); regeo = false; break;
             case SC_OPT_INTEGRAL_PRE: o.integral_pre = range(0, 64); regeo = false; break;
-            case SC_OPT_INTEGRAL_ONE: o.integral_one = range(0, 1); regeo = false; break;
             case SC_OPT_TEST_DROP_HANDOFF:
 #if !defined(SC_TEST_HOOKS) || !SC_TEST_HOOKS
                 if (value != -1) throw Error{SC_ERR_INVALID, "test_drop_handoff needs the test-hook build (lib/testhooks)"};

@@ -110,21 +110,13 @@ __device__ __forceinline__ uint32_t byte_of(unsigned long long w, int i) {
     return (uint32_t)(w >> (8 * i)) & 0xffu;
 }
 
-// Row y of frame `frame`.  PUB (the one-frame integral kernel): the R row's
-// cells are stored write-through (buffer stores with sc1) and, once every
-// store of the wave has drained, the row is published: rowflag[y] = epoch
-// (agent scope; the column walks of the same launch poll it, Guideline 16
-// R1, as the chain kernel's fused walks do).  zi0 / znt: this row's share of
-// the step's zeroed int arrays (first index, stride).
-template <bool PUB>
-__device__ __forceinline__ void rowcarry4_row(const RowScanArgs &a, int y, int frame, long long zi0, long long znt,
-                                              int epoch, int *rowflag) {
-    const int lane = threadIdx.x;
+__global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
+    const int y = blockIdx.x, frame = blockIdx.y, lane = threadIdx.x;
     const TableGeom g = a.g;
     const int W = g.W, H = g.H, ns = (W + kStrip - 1) / kStrip;
     {   // the step's zeroed int arrays, grid-strided over the workgroups
-        const long long nt = znt;
-        const long long i0 = zi0 + lane;
+        const long long nt = (long long)gridDim.x * gridDim.y * 64;
+        const long long i0 = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 64 + lane;
 #pragma unroll
         for (int k = 0; k < 4; k++)
             for (long long i = i0; i < a.zero_n[k]; i += nt) a.zero[k][i] = 0;
@@ -221,19 +213,8 @@ __device__ __forceinline__ void rowcarry4_row(const RowScanArgs &a, int y, int f
                     r0.z = run[2] + (e[1] & 0xffffu) + Pc[j][2]; r0.w = run[3] + (e[1] >> 16) + Pc[j][3];
                     r1.x = run[4] + (e[2] & 0xffffu) + Pc[j][4]; r1.y = run[5] + (e[2] >> 16) + Pc[j][5];
                     r1.z = run[6] + (e[3] & 0xffffu) + Pc[j][6]; r1.w = run[7] + (e[3] >> 16) + Pc[j][7];
-                    if constexpr (PUB) {  // write-through: the walks of this launch read them on other XCDs
-                        typedef unsigned v4u __attribute__((ext_vector_type(4)));
-                        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                            tab, (short)0, (int)(g.frame4 * 16), 0x00020000);
-                        const unsigned ob = (unsigned)((long long)(y + 1) * g.rowp) * 16u;
-                        __builtin_amdgcn_raw_buffer_store_b128(v4u{r0.x, r0.y, r0.z, r0.w}, rs,
-                                                               (int)(ob + (unsigned)g.at(x + 1, 0) * 16u), 0, 16);
-                        __builtin_amdgcn_raw_buffer_store_b128(v4u{r1.x, r1.y, r1.z, r1.w}, rs,
-                                                               (int)(ob + (unsigned)g.at(x + 1, 1) * 16u), 0, 16);
-                    } else {
-                        reinterpret_cast<uint4 *>(trow)[g.at(x + 1, 0)] = r0;
-                        reinterpret_cast<uint4 *>(trow)[g.at(x + 1, 1)] = r1;
-                    }
+                    reinterpret_cast<uint4 *>(trow)[g.at(x + 1, 0)] = r0;
+                    reinterpret_cast<uint4 *>(trow)[g.at(x + 1, 1)] = r1;
                 }
             }
         }
@@ -254,17 +235,6 @@ __device__ __forceinline__ void rowcarry4_row(const RowScanArgs &a, int y, int f
         ld = (uint32_t)__builtin_amdgcn_readlane((int)d0, 63) >> 24;
         u0 = u1; c0 = c1; d0 = d1;
     }
-    if constexpr (PUB) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every store of this wave drained
-        const unsigned long long ex = __ballot(1);
-        if (__builtin_amdgcn_mbcnt_hi((unsigned)(ex >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ex, 0u)) == 0u)
-            __hip_atomic_store(&rowflag[y], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-__global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
-    rowcarry4_row<false>(a, blockIdx.x, blockIdx.y, ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 64,
-                         (long long)gridDim.x * gridDim.y * 64, 0, nullptr);
 }
 
 #ifndef SC_COL_XCD
@@ -416,110 +386,34 @@ __global__ __launch_bounds__(64) void colsum_kernel(RowScanArgs a) {
 #define SC_SUM_AHEAD4 48
 #endif
 constexpr int kSumAhead4 = SC_SUM_AHEAD4;
-// Column walk `lb` (of nb per frame): 16 columns x 4 channels of one half,
-// S += (float)R_y down each column in colstrip's order.  WAIT (the one-frame
-// integral kernel): before loading rows it polls the rows' flags (rowcarry4
-// rows of the same launch, published with epoch) 64 at a time and takes an
-// agent-scope acquire; a row that never arrives (0.5 s) counts in *err and
-// the walk goes on (the call then fails, never hangs).
-template <bool WAIT>
-__device__ __forceinline__ void colsum4_walk(const RowScanArgs &a, int lb, int nb, int epoch, const int *rowflag,
-                                             int *err) {
-    const int frame = lb / nb, rem = lb - frame * nb;
-    const int s = rem >> 3, h = (rem >> 2) & 1, sub = rem & 3, lane = threadIdx.x;
-    const TableGeom g = a.g;
-    const int W = g.W, H = g.H;
-    const int x = s * 2 * kStrip + sub * 16 + (lane >> 2), ch = lane & 3;
-    const bool live = x < W;  // (dead lanes stay for the polls' ballots)
-    float *cellp = reinterpret_cast<float *>(a.table + (long long)frame * g.frame4 + g.at((live ? x : W - 1) + 1, h) +
-                                             g.rowp) + ch;
-    const uint32_t *rp = reinterpret_cast<const uint32_t *>(cellp);
-    const long long rs = (long long)g.rowp * 4;  // floats per table row
-    int wm = 0;  // rows below wm are published and acquired (WAIT)
-    auto ready = [&](int hi) {
-        if constexpr (WAIT) {
-            hi = min(hi, H);
-            if (wm >= hi) return;
-            unsigned long long t0 = 0;
-            while (wm < hi) {
-                const int yy = wm + lane;
-                int f = epoch;
-                if (yy < H) f = __hip_atomic_load(&rowflag[yy], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned long long ok = __ballot(f == epoch);
-                const int adv = ~ok ? __builtin_ctzll(~ok) : 64;
-                if (adv == 0) {
-                    __builtin_amdgcn_s_sleep(2);
-                    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-                    if (!t0) t0 = t;
-                    else if (t - t0 > 50000000ull) {  // 0.5 s: a lost row (never expected)
-                        if (err && lane == 0) atomicAdd(err, 1);
-                        wm = hi;
-                        break;
-                    }
-                    continue;
-                }
-                wm = min(H, wm + adv);
-            }
-            // (no acquire fence: an agent-scope acquire invalidates the L2;
-            // the R rows are read below with sc1 loads, which go past the
-            // caches to where the rows' sc1 stores went)
-            asm volatile("" ::: "memory");
-        }
-    };
-    // R of row y: table row y + 1 (WAIT: sc1 buffer loads)
-    const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float4 *>(a.table + (long long)frame * g.frame4), (short)0, (int)(g.frame4 * 16), 0x00020000);
-    const unsigned rb0 = (unsigned)((const char *)rp - (const char *)(a.table + (long long)frame * g.frame4));
-    auto ld_r = [&](int y) -> uint32_t {
-        if constexpr (WAIT)
-            return (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsr, (int)(rb0 + (unsigned)(y * rs) * 4u), 0, 16);
-        else
-            return rp[y * rs];
-    };
-    float S = 0.0f;
-    uint32_t ra[kSumAhead4];
-    ready(kSumAhead4);
-#pragma unroll
-    for (int k = 0; k < kSumAhead4; k++) ra[k] = ld_r(min(k, H - 1));
-    for (int y0 = 0; y0 < H; y0 += kSumAhead4) {
-        uint32_t rb[kSumAhead4];
-        ready(y0 + 2 * kSumAhead4);
-#pragma unroll
-        for (int k = 0; k < kSumAhead4; k++) rb[k] = ld_r(min(y0 + kSumAhead4 + k, H - 1));
-#pragma unroll
-        for (int k = 0; k < kSumAhead4; k++) {
-            S = S + (float)ra[k];  // the f32 column step, colstrip's order
-            if (live && y0 + k < H) cellp[(y0 + k) * rs] = S;
-        }
-#pragma unroll
-        for (int k = 0; k < kSumAhead4; k++) ra[k] = rb[k];
-    }
-}
-
 __global__ __launch_bounds__(64) void colsum4_kernel(RowScanArgs a) {
     const int nb = gridDim.x * gridDim.y, b = blockIdx.x + blockIdx.y * gridDim.x;
     const int xq = b % kXcds, q = nb / kXcds, r = nb % kXcds;
     const int lb = xq * q + min(xq, r) + b / kXcds;  // XCD-aware: neighbours through one L2
-    colsum4_walk<false>(a, lb, gridDim.x, 0, nullptr, nullptr);
-}
-
-// The one-frame integral in ONE launch (two-pass form, rowcarry4 + colsum4):
-// workgroups [0, nwalk) are colsum4's column walks, the others rowcarry4's
-// rows, which publish each R row as it is written; the walks follow the rows
-// down (per-row flags, epoch-tagged so nothing is reset between calls).  The
-// same f32 operations in the same order as the two kernels: bit-identical.
-// Every workgroup of the launch is co-resident (nwalk + H single-wave
-// workgroups, checked by the host against the occupancy limit), so the
-// walks' waits always end.
-__global__ __launch_bounds__(64) void integral1_kernel(RowScanArgs a, int nwalk, int epoch, int *rowflag,
-                                                       int *err) {
-    const int b = blockIdx.x;
-    if (b < nwalk) {
-        const int xq = b % kXcds, q = nwalk / kXcds, r = nwalk % kXcds;
-        colsum4_walk<true>(a, xq * q + min(xq, r) + b / kXcds, nwalk, epoch, rowflag, err);
-    } else {
-        const int rows = gridDim.x - nwalk;
-        rowcarry4_row<true>(a, b - nwalk, 0, (long long)(b - nwalk) * 64, (long long)rows * 64, epoch, rowflag);
+    const int frame = lb / gridDim.x, rem = lb - frame * gridDim.x;
+    const int s = rem >> 3, h = (rem >> 2) & 1, sub = rem & 3, lane = threadIdx.x;
+    const TableGeom g = a.g;
+    const int W = g.W, H = g.H;
+    const int x = s * 2 * kStrip + sub * 16 + (lane >> 2), ch = lane & 3;
+    if (x >= W) return;  // (no cross-lane work in this pass)
+    float *cellp = reinterpret_cast<float *>(a.table + (long long)frame * g.frame4 + g.at(x + 1, h) + g.rowp) + ch;
+    const uint32_t *rp = reinterpret_cast<const uint32_t *>(cellp);
+    const long long rs = (long long)g.rowp * 4;  // floats per table row
+    float S = 0.0f;
+    uint32_t ra[kSumAhead4];
+#pragma unroll
+    for (int k = 0; k < kSumAhead4; k++) ra[k] = rp[min(k, H - 1) * rs];
+    for (int y0 = 0; y0 < H; y0 += kSumAhead4) {
+        uint32_t rb[kSumAhead4];
+#pragma unroll
+        for (int k = 0; k < kSumAhead4; k++) rb[k] = rp[min(y0 + kSumAhead4 + k, H - 1) * rs];
+#pragma unroll
+        for (int k = 0; k < kSumAhead4; k++) {
+            S = S + (float)ra[k];  // the f32 column step, colstrip's order
+            if (y0 + k < H) cellp[(y0 + k) * rs] = S;
+        }
+#pragma unroll
+        for (int k = 0; k < kSumAhead4; k++) ra[k] = rb[k];
     }
 }
 
@@ -577,22 +471,6 @@ bool launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
     b.rfull_n = 0;
     hipLaunchKernelGGL(rowcarry_kernel, dim3((a.g.H + kRcRows - 1) / kRcRows, n_frames), dim3(64 * kRcRows), 0, s, b);
     return false;
-}
-
-bool launch_integral1(const RowScanArgs &a, int epoch, int *rowflag, int *err, hipStream_t s) {
-    const bool aligned = ((uintptr_t)a.frames & 3u) == 0 && (a.stride & 3) == 0;
-    if (!SC_RC_DWORD || !aligned || a.rfull_n < 1) return false;
-    const int ns64 = (a.g.W + 2 * kStrip - 1) / (2 * kStrip), nwalk = ns64 * 8;
-    const int blocks = nwalk + a.g.H;
-    // every workgroup must be resident at once (the walks wait on rows)
-    int per_cu = 0, cus = 0, dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, integral1_kernel, 64, 0) != hipSuccess ||
-        (long long)per_cu * cus < blocks)
-        return false;
-    hipLaunchKernelGGL(integral1_kernel, dim3(blocks), dim3(64), 0, s, a, nwalk, epoch, rowflag, err);
-    return true;
 }
 
 void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s, bool have_r) {

@@ -245,11 +245,6 @@ void launch_features(const FeatureArgs &a, hipStream_t s);
 bool launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s);
 // two_pass: rowfull + colsum (small batches; rowfull skipped when have_r), else colstrip
 void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s, bool have_r = false);
-// One frame, two-pass form: rowcarry4's rows and colsum4's walks in one
-// launch (per-row flags tagged with `epoch`, rowflag[H], never reset).
-// False (nothing launched) when the frame is not 4-B aligned or the launch
-// cannot be co-resident.
-bool launch_integral1(const RowScanArgs &a, int epoch, int *rowflag, int *err, hipStream_t s);
 // Per-detector launch configuration: the device's CU count (queried once
 // per detector, no process-wide cache) and the SC_OPT_* launch options.
 struct LaunchCfg {

@@ -95,7 +95,7 @@ __device__ __forceinline__ int lane_id() {
 // lane 0 is active at every such site; a dequeue whose atomic lane is
 // inactive returns task 0 forever (readfirstlane then reads a lane that
 // never did the atomic): the livelock shape of round 3's hang (DESIGN.md
-// section 5b, "walker hang").
+// section 6a).
 __device__ __forceinline__ bool lead_lane() {
     const unsigned long long ex = __ballot(1);
     return __builtin_amdgcn_mbcnt_hi((unsigned)(ex >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ex, 0u)) == 0u;

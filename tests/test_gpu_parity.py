@@ -44,26 +44,6 @@ def test_integral_bit_exact(sc, oracle, W, H, seed, layout, passes):
     assert T.view(np.uint32).tobytes() == ref.view(np.uint32).tobytes()
 
 
-@pytest.mark.parametrize("W,H", [(640, 480), (1920, 1080), (257, 131), (2, 2), (3000, 67), (3840, 2160)])
-def test_integral_one_launch(sc, oracle, W, H):
-    """One-frame calls build the integral in ONE launch (integral1: rowcarry4's
-    rows publish their R rows, colsum4's walks follow them down; per-row
-    flags tagged by call, never reset): bit-exact for several calls on one
-    detector with different frames (stale flags of earlier calls must not
-    pass), and equal to the two-launch form (SC_OPT_INTEGRAL_ONE 1)."""
-    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1))
-    two = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1)).set_option("integral_one", 1)
-    for seed in (11, 12, 13):
-        img = _frame(W, H, seed)
-        det.detect(img)
-        assert det.info("column_pass") == 3
-        ref = oracle.integral(img)
-        assert det.dump_integral(W, H).view(np.uint32).tobytes() == ref.view(np.uint32).tobytes()
-        two.detect(img)
-        assert two.info("column_pass") == 1
-        assert two.dump_integral(W, H).view(np.uint32).tobytes() == ref.view(np.uint32).tobytes()
-
-
 def _grid_parity(sc, oracle, cascade, cfg, img, params_sc, params_or, model_text=None, det_out=None, **opts):
     det = sc.Detector(sc.Model.parse(model_text) if model_text else cfg, params_sc).set_options(**opts)
     if det_out is not None:
@@ -397,7 +377,7 @@ def test_integral_device_pitch(sc, oracle, pitch, off):
     import torch
     W, H = 641, 301
     rng = np.random.default_rng(pitch + off)
-    for n in (1, 3, 5):  # (1: the one-launch integral when aligned)
+    for n in (3, 5):
         buf = rng.integers(0, 256, (n, H, pitch), dtype=np.uint8)
         view = buf[:, :, off:off + W]
         det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=2))
