@@ -583,3 +583,48 @@ def test_grid_parity_extreme_content(sc, oracle, face_cascade, kind):
            else np.random.default_rng(11).integers(0, 256, (H, W))).astype(np.uint8)
     _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=5),
                  oracle.Params(n_levels=5))
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_random_geometry_sweep(sc, oracle, face_cascade, case):
+    """Seeded random sweep over what the chain kernel's segmenting, hand-offs,
+    integral forms and speculation depend on: frame size (ragged rows and
+    strips), level count, base window, step, prefilter factor, stride
+    threshold, thetas (permissive or the model's) and frames per call (1: two
+    launches and speculation; 2-3: two-pass; 4-5: fused walks).  Every frame:
+    evaluated windows, visited set and detections equal the oracle's."""
+    from surfcascade_amd import synth
+    rng = np.random.default_rng(700 + case)
+    W, H = int(rng.integers(90, 720)), int(rng.integers(90, 540))
+    base = int(rng.choice([40, 48, 56, 70]))
+    step = int(rng.choice([0, 1, 2, 3, 5]))
+    pk = float(rng.choice([3.0, 6.0, 9.0]))
+    ss = float(rng.choice([0.3, 0.5, 0.7]))
+    n = int(rng.integers(1, 6))
+    levels = int(rng.integers(1, 7))
+    c = face_cascade
+    theta = np.full(c.n_stages, 0.4, np.float32) if case % 2 else c.theta
+    text = synth.write_cfg(synth.cascade_tree(c.n_weak, theta, c.patch_index, c.w, c.bias))
+    casc = oracle.cascade_from_cfg(text)
+    prm_sc = sc.ScanParams(base_len=base, step=step, prefilter_k=pk, stride_score=ss, n_levels=levels)
+    prm_or = oracle.Params(base_len=base, step=step, prefilter_k=pk, stride_score=ss, n_levels=levels)
+    frames = np.stack([_frame(W, H, 5000 + 13 * case + k) for k in range(n)])
+    det = sc.Detector(sc.Model.parse(text), prm_sc)
+    det.set_debug(True)
+    batch = det.detect_batch(frames, capacity=1 << 18)
+    layout, _ = oracle.grid_layout(W, H, prm_or)
+    nvis_all = 0
+    for k in range(n):
+        T = oracle.integral(frames[k])
+        assert det.dump_integral(W, H, frame=k).view(np.uint32).tobytes() == T.view(np.uint32).tobytes()
+        p, s, v = det.dump_grid(frame=k)
+        rp, rs = oracle.eval_grid(T, casc, prm_or)
+        ev = p != -2
+        np.testing.assert_array_equal(p[ev], rp[ev])
+        assert s[ev].view(np.uint32).tobytes() == rs[ev].view(np.uint32).tobytes()
+        rv, _ = oracle.walk_grid(rp, rs, layout, casc.n_stages, prm_or.stride_score)
+        np.testing.assert_array_equal(v, rv)
+        ref, nvis = oracle.detect(T, casc, prm_or)
+        assert _det_set(batch[k]) == _det_set(ref)
+        nvis_all += nvis
+    assert det.info("visited") == nvis_all
