@@ -795,6 +795,78 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_ldsgather(Args a) {
     }
 }
 
+// V15 (round 4): the production item with every corner fetched by LDS DMA
+// (global_load_lds_dwordx4: per-lane source, the wave's 1 KiB lands
+// lane-linear in its LDS slot) and read back with a conflict-free
+// ds_read_b128 at lane*16: does routing the gathers' data into LDS instead of
+// VGPRs relieve the texture data path (TD ~97 % busy in the chain kernel)?
+// Same corners, same arithmetic: bit-exact with V0.
+template <class P>
+__device__ __forceinline__ void features_dma(const char *Tb, unsigned off, int half_off, const P &pj,
+                                             float4 *slot, f2 (&fp)[16]) {
+    int co[10];
+    corner_offsets(pj, co);
+    const int lane = threadIdx.x & 63;
+    f2 h[2][8];
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++) {
+#pragma unroll
+        for (int m = 0; m < 10; m++)
+            __builtin_amdgcn_global_load_lds(
+                (const __attribute__((address_space(1))) void *)(Tb + (off + ((unsigned)(hh * half_off + co[m]) << 4))),
+                (__attribute__((address_space(3))) void *)(slot + m * 64), 16, 0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        float4 cn[10];
+#pragma unroll
+        for (int m = 0; m < 10; m++) cn[m] = slot[m * 64 + lane];
+        half_box(pj.shape, cn, h[hh]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot reads done before the next half's DMA
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        fp[4 * c] = h[0][2 * c];
+        fp[4 * c + 1] = h[0][2 * c + 1];
+        fp[4 * c + 2] = h[1][2 * c];
+        fp[4 * c + 3] = h[1][2 * c + 1];
+    }
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_dma(Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4 *Wl; double *Bl; int4 *Rl; float *Sc;
+    stage<WAVES>(a, smem, Wl, Bl, Rl, Sc);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float4 *slot = reinterpret_cast<float4 *>(smem + (((size_t)a.K * (144 + 8 + 16) + a.n_levels * 4 + 63) & ~(size_t)63)) +
+                   (size_t)wv * 10 * 64;
+    const int lane = threadIdx.x & 63;
+    const unsigned q0 = xcc();
+    const char *Tb = reinterpret_cast<const char *>(a.table);
+    for (unsigned qi = 0; qi < 8; qi++) {
+      const unsigned q = (q0 + qi) & 7;
+      const Item *I = a.items + q * a.cap;
+      float *O = a.out + q * a.cap;
+      const int n = a.n_items[q];
+      for (;;) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&a.tickets[q * 64], 1);
+        b0 = __builtin_amdgcn_readfirstlane(b0) * kChunk * kBlock;
+        if (b0 >= n) break;
+        const int b1 = min(n, b0 + kChunk * kBlock);
+        for (int i0 = b0; i0 < b1; i0 += 64) {  // (the whole wave runs every iteration: the DMA needs it)
+            const int i = i0 + lane;
+            const bool live = i < b1;
+            const Item it = I[live ? i : b0];
+            f2 fp[16];
+            features_dma(Tb, it.origin << 4, a.g.hs, project(a, Rl, Sc, it), slot, fp);
+            normalize2(fp);
+            const float o = lr_predict2(fp, Wl + it.k * 9, Bl[it.k]);
+            if (live) O[i] = o;
+        }
+      }
+    }
+}
+
 }  // namespace
 
 extern "C" int ib_run(int variant, int waves, const Args *a, void *stream) {
@@ -838,6 +910,11 @@ extern "C" int ib_run(int variant, int waves, const Args *a, void *stream) {
         const size_t lt = ((lds + 63) & ~(size_t)63) + kTileCells * 16;
         if (waves == 12) hipLaunchKernelGGL((k_ldsgather<12>), dim3(cus), dim3(768), lt, s, *a);
         else if (waves == 16) hipLaunchKernelGGL((k_ldsgather<16>), dim3(cus), dim3(1024), lt, s, *a);
+        else return -1;
+    } else if (variant == 15) {  // corners by LDS DMA: + 10 KiB per wave
+        const size_t lt = ((lds + 63) & ~(size_t)63) + (size_t)waves * 10 * 1024;
+        if (waves == 8) hipLaunchKernelGGL((k_dma<8>), dim3(cus), dim3(512), lt, s, *a);
+        else if (waves == 12) hipLaunchKernelGGL((k_dma<12>), dim3(cus), dim3(768), lt, s, *a);
         else return -1;
     } else if (variant == 3) {
         if (waves == 8) L(k_fold, 8); else if (waves == 12) L(k_fold, 12); else if (waves == 16) L(k_fold, 16); else return -1;

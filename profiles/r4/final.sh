@@ -16,3 +16,9 @@ cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv \
     -d $R/$O/calib_pmc -o pmc -- $R/profiles/calib/fetch_calib > $R/$O/calib_pmc.txt 2>&1 || exit 1
 echo final done
+# the LDS-DMA item variant (itembench V15) against the production item
+bash profiles/run.sh r4final "itembench --reps 5 --variants 0:12,15:12,0:8,15:8" || exit 1
+cd /tmp && timeout -s KILL 120 rocprofv3 --pmc TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE SQ_LDS_IDX_ACTIVE --kernel-trace \
+    --output-format csv -d $R/$O/ib15_td -o pmc -- python3 $R/profiles/itembench/run.py --reps 1 --variants 0:12,15:12 \
+    > $R/$O/ib15_td.txt 2>&1 || exit 1
+echo ib15 done
