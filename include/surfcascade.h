@@ -219,7 +219,8 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
 #define SC_OPT_SUBSTRIPS 5    /* full grid: strips per XCD band (0 auto)       */
 #define SC_OPT_BAND_ROWS 6    /* full grid: grid rows per task band (0: 1)     */
 #define SC_OPT_ROW_ORDER 7    /* chain tasks: 0 level-major, 1 y-major,        */
-                              /* 2 blocks of ROW_BLOCK grid rows (default)     */
+                              /* 2 blocks of ROW_BLOCK grid rows (default),    */
+                              /* 3 the same blocks bottom-up                   */
 #define SC_OPT_ROW_BLOCK 8    /* grid rows per block (default 32)              */
 #define SC_OPT_CHAIN_CHUNK 9  /* frames per chain-kernel launch at most (0:    */
                               /* as many as 32-bit table offsets allow)        */

@@ -446,6 +446,9 @@ void build_geometry(sc_detector *d, int W, int H) {
         else if (mode == 2)
             std::stable_sort(ng.rows.begin(), ng.rows.end(),
                              [blk](const int2 &a, const int2 &b) { return a.y / blk < b.y / blk; });
+        else if (mode == 3)  // the blocks bottom-up: the last block dealt holds every level's top rows
+            std::stable_sort(ng.rows.begin(), ng.rows.end(),
+                             [blk](const int2 &a, const int2 &b) { return a.y / blk > b.y / blk; });
     }
     d->d_tasks.ensure(std::max<size_t>(ng.tasks.size(), 1));
     if (!ng.tasks.empty())
@@ -1538,7 +1541,7 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
             case SC_OPT_PHASES: o.phases = range(0, 2); break;
             case SC_OPT_SUBSTRIPS: o.substrips = range(0, 64); break;
             case SC_OPT_BAND_ROWS: o.band_rows = range(0, 64); break;
-            case SC_OPT_ROW_ORDER: o.row_order = range(0, 2); break;
+            case SC_OPT_ROW_ORDER: o.row_order = range(0, 3); break;
             case SC_OPT_ROW_BLOCK: o.row_block = range(1, 1 << 16); break;
             case SC_OPT_CHAIN_CHUNK: o.chain_chunk = range(0, 1 << 20); regeo = false; break;
             case SC_OPT_LDS_WEIGHTS: o.lds_weights = range(-1, 1); regeo = false; break;
