@@ -362,6 +362,8 @@ def main():
         k, v = o.split("=", 1)
         opts[k] = int(v)
     det.set_options(**opts)
+    if not stub:  # launches on torch's current stream: stream-ordered with the bench's tensors, no event pair per call
+        det.set_stream(torch.cuda.current_stream(dev))
     if grid_shard:
         det.set_shard(rank, world)
     # record buffers: grown (every rank, same size) whenever a scan finds more

@@ -141,6 +141,13 @@ void *sc_detector_stream(sc_detector *d); /* hipStream_t */
  * SC_ERR_INVALID otherwise). */
 int sc_detector_wait_stream(sc_detector *d, void *stream);
 int sc_stream_wait_detector(sc_detector *d, void *stream);
+/* Launch on the caller's stream instead (a stream of the detector's GPU, NULL
+ * = HIP's null stream), or back on the detector's own (use_own != 0, stream
+ * ignored).  Work on the caller's stream is then ordered with the detector's
+ * without the two calls above (one event pair less per call).  The switch is
+ * ordered: work queued after it waits for the detector's work queued before
+ * it.  The caller keeps the stream alive while it is set. */
+int sc_detector_set_stream(sc_detector *d, void *stream, int use_own);
 
 /* ---- hard-negative mining (training side) ----------
  * DenseSURFFeatureExtractor::FillNegSamples' scan of one negative image

@@ -57,7 +57,7 @@ EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_mode
            "sc_extract_patches", "sc_detector_create", "sc_detector_create_from_model",
            "sc_detector_destroy", "sc_detect", "sc_detect_batch", "sc_detect_device",
            "sc_enqueue_device", "sc_synchronize", "sc_detector_stream", "sc_detector_wait_stream",
-           "sc_stream_wait_detector", "sc_detector_info",
+           "sc_stream_wait_detector", "sc_detector_set_stream", "sc_detector_info",
            "sc_detector_set_shard", "sc_detector_set_option", "sc_detector_set_debug", "sc_debug_dump", "sc_set_timing", "sc_get_timing",
            "sc_group_rectangles", "sc_group_detections", "sc_fddb_format",
            "sc_miner_create", "sc_mine", "sc_mine_device", "sc_mine_batch", "sc_mine_batch_device", "sc_fast_nms", "sc_decode_jpeg_gray", "sc_imread_gray",
@@ -148,6 +148,7 @@ def load_library():
     L.sc_detector_stream.restype = vp
     L.sc_detector_wait_stream.argtypes = [vp, vp]
     L.sc_stream_wait_detector.argtypes = [vp, vp]
+    L.sc_detector_set_stream.argtypes = [vp, vp, ctypes.c_int]
     L.sc_detector_info.argtypes = [vp, i32, P(i64)]
     L.sc_detector_set_debug.argtypes = [vp, i32]
     L.sc_detector_set_shard.argtypes = [vp, i32, i32]
@@ -483,13 +484,15 @@ class Detector:
             if t is not None and (not t.is_cuda or t.device.index != self.device):
                 raise ValueError("tensor on %s, detector on cuda:%d" % (t.device, self.device))
         s = torch.cuda.current_stream(self.device).cuda_stream
-        _check(load_library().sc_detector_wait_stream(self._h, s))
+        if s != (self.stream_ptr or 0):  # (a detector on torch's current stream is ordered already)
+            _check(load_library().sc_detector_wait_stream(self._h, s))
 
     def _before_torch(self):
         """Order torch's current stream after the detector's queued work."""
         import torch
         s = torch.cuda.current_stream(self.device).cuda_stream
-        _check(load_library().sc_stream_wait_detector(self._h, s))
+        if s != (self.stream_ptr or 0):
+            _check(load_library().sc_stream_wait_detector(self._h, s))
 
     def detect_device(self, frames, capacity=1 << 18):
         n, H, W, rs = self._device_frames(frames)
@@ -523,6 +526,17 @@ class Detector:
     @property
     def stream_ptr(self):
         return load_library().sc_detector_stream(self._h)
+
+    def set_stream(self, stream=None):
+        """Launch on `stream` (a torch.cuda.Stream, or a raw hipStream_t of the
+        detector's GPU, 0 = the null stream; None: the detector's own stream).
+        On torch's current stream, enqueue_device needs no stream-order events
+        (sc_detector_set_stream)."""
+        if stream is None:
+            _check(load_library().sc_detector_set_stream(self._h, None, 1))
+        else:
+            ptr = int(getattr(stream, "cuda_stream", stream))
+            _check(load_library().sc_detector_set_stream(self._h, ptr or None, 0))
 
     # -- introspection ---------------------------------------------------------
     def info(self, key):

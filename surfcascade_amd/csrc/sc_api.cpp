@@ -97,7 +97,8 @@ struct Geometry {
     sc::TableGeom tg{};
     long long grid = 0;
     std::vector<sc::LevelInfo> levels;
-    std::vector<int2> rows;
+    std::vector<int2> rows;   // chain kernel task order (rows1: one-frame launches)
+    std::vector<int2> rows1;
     std::vector<sc::ProjPatch> proj;
     std::vector<sc::ProjPatch> proj_all;  // miner: every template patch per level
     std::vector<sc::TaskDesc> tasks;
@@ -107,7 +108,8 @@ struct Geometry {
 
 struct sc_detector {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // where launches go: own_stream, or the caller's (sc_detector_set_stream)
+    hipStream_t own_stream = nullptr;  // created with the detector, destroyed with it
     sc_scan_params prm{};
     sc::Cascade casc;
     int K = 0, S = 0;
@@ -126,6 +128,7 @@ struct sc_detector {
     struct Options {
         int full_grid = 0, chunk_min = 0, table_layout = 0, phases = 0, substrips = 0;
         int band_rows = 0, row_order = 2, row_block = 32, chain_chunk = 0;
+        bool order_set = false;  // ROW_ORDER / ROW_BLOCK set: one-frame launches use them too
         int lds_weights = -1, wgs_per_cu = 0, profile = 0, chain_segs = 0, integral_passes = 0;
         int level_lo = 0, level_hi = 0;  // scan only levels [lo, hi) (hi 0: all)
         int chain_waves = 0;             // chain kernel waves per workgroup (0 auto)
@@ -167,6 +170,7 @@ struct sc_detector {
     // touch it, so a timeout in any pipelined step is still raised at the
     // next synchronisation); zeroed once at allocation and after each read
     DevBuf<int> d_err;
+    int *h_err = nullptr;  // its raised flag, mapped host memory the kernel writes (check_chain)
     bool chain_launched = false;  // a chain launch since the last check_chain
     DevBuf<int8_t> d_st_p;      // per grid window: stage reached (-1 prefilter reject)
     DevBuf<float> d_st_s;       // per grid window: last stage score
@@ -192,6 +196,7 @@ struct sc_detector {
     ~sc_detector() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
+        if (own_stream && own_stream != stream) (void)hipStreamSynchronize(own_stream);
         for (auto &p : pending) {
             event_pool.push_back(p.a);
             event_pool.push_back(p.b);
@@ -206,7 +211,8 @@ struct sc_detector {
         d_visited.release(); d_queues.release(); d_entry.release(); d_err.release(); d_st_p.release(); d_st_s.release();
         d_dbg_v.release(); d_prof.release();
         h_stage.release();
-        if (stream) (void)hipStreamDestroy(stream);
+        if (h_err) (void)hipHostFree(h_err);
+        if (own_stream) (void)hipStreamDestroy(own_stream);
     }
 
     hipEvent_t ev() {
@@ -437,33 +443,45 @@ void build_geometry(sc_detector *d, int W, int H) {
         // rows that fits its L2: 14 % less kernel time than plain level-major
         // order (0) on the C2 frames; blocks of 64 rows 1 % and of 128 rows
         // 3 % slower than 32 (profiles/r1/sweep); 1: y-major.
+        // One-frame launches deal a second list (rows1): blocks of 8 grid rows
+        // bottom-up (3), so the last block dealt holds every level's top rows
+        // and the wide levels' short rows end the launch: chain kernel 0.606
+        // vs 0.614 ms (profiles/r4/order/); SC_OPT_ROW_ORDER / _ROW_BLOCK set
+        // explicitly apply to both lists.
         // (The full-grid tasks above are built from the level-major list.)
-        const int mode = d->opt.row_order;  // SC_OPT_ROW_ORDER / SC_OPT_ROW_BLOCK
-        const int blk = d->opt.row_block * ng.step;
-        if (mode == 1)
-            std::stable_sort(ng.rows.begin(), ng.rows.end(),
-                             [](const int2 &a, const int2 &b) { return a.y < b.y; });
-        else if (mode == 2)
-            std::stable_sort(ng.rows.begin(), ng.rows.end(),
-                             [blk](const int2 &a, const int2 &b) { return a.y / blk < b.y / blk; });
-        else if (mode == 3)  // the blocks bottom-up: the last block dealt holds every level's top rows
-            std::stable_sort(ng.rows.begin(), ng.rows.end(),
-                             [blk](const int2 &a, const int2 &b) { return a.y / blk > b.y / blk; });
+        auto order = [&](std::vector<int2> rows, int mode, int blk) {
+            if (mode == 1)
+                std::stable_sort(rows.begin(), rows.end(),
+                                 [](const int2 &a, const int2 &b) { return a.y < b.y; });
+            else if (mode == 2)
+                std::stable_sort(rows.begin(), rows.end(),
+                                 [blk](const int2 &a, const int2 &b) { return a.y / blk < b.y / blk; });
+            else if (mode == 3)
+                std::stable_sort(rows.begin(), rows.end(),
+                                 [blk](const int2 &a, const int2 &b) { return a.y / blk > b.y / blk; });
+            return rows;
+        };
+        ng.rows1 = d->opt.order_set ? order(ng.rows, d->opt.row_order, d->opt.row_block * ng.step)
+                                    : order(ng.rows, 3, 8 * ng.step);
+        ng.rows = order(ng.rows, d->opt.row_order, d->opt.row_block * ng.step);
     }
     d->d_tasks.ensure(std::max<size_t>(ng.tasks.size(), 1));
     if (!ng.tasks.empty())
         HIPCHK(hipMemcpyAsync(d->d_tasks.p, ng.tasks.data(), ng.tasks.size() * sizeof(sc::TaskDesc),
                               hipMemcpyHostToDevice, d->stream));
     d->d_levels.ensure(std::max<size_t>(ng.levels.size(), 1));
-    d->d_rows.ensure(std::max<size_t>(ng.rows.size(), 1));
+    d->d_rows.ensure(std::max<size_t>(2 * ng.rows.size(), 1));  // [rows | rows1]
     d->d_proj.ensure(std::max<size_t>(ng.proj.size(), 1));
     if (!ng.levels.empty())
         HIPCHK(hipMemcpyAsync(d->d_levels.p, ng.levels.data(),
                               ng.levels.size() * sizeof(sc::LevelInfo), hipMemcpyHostToDevice,
                               d->stream));
-    if (!ng.rows.empty())
+    if (!ng.rows.empty()) {
         HIPCHK(hipMemcpyAsync(d->d_rows.p, ng.rows.data(), ng.rows.size() * sizeof(int2),
                               hipMemcpyHostToDevice, d->stream));
+        HIPCHK(hipMemcpyAsync(d->d_rows.p + ng.rows.size(), ng.rows1.data(), ng.rows1.size() * sizeof(int2),
+                              hipMemcpyHostToDevice, d->stream));
+    }
     if (!ng.proj.empty())
         HIPCHK(hipMemcpyAsync(d->d_proj.p, ng.proj.data(), ng.proj.size() * sizeof(sc::ProjPatch),
                               hipMemcpyHostToDevice, d->stream));
@@ -584,7 +602,8 @@ sc_detector *make_detector(const sc::Cascade &c, const sc_scan_params *p, int de
         d->miner = miner;
         if (miner) d->all_rects = sc::extract_patches(prm.tmpl_w, prm.tmpl_h);
         HIPCHK(hipDeviceGetAttribute(&d->cus, hipDeviceAttributeMultiprocessorCount, device));
-        HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&d->own_stream, hipStreamNonBlocking));
+        d->stream = d->own_stream;
         upload_model(d);
     } catch (...) {
         delete d;
@@ -652,6 +671,11 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     if (chain) {
         d->d_entry.ensure((size_t)entry_words(std::min(chunk, n)));
         if (!d->d_err.p) {
+            if (!d->h_err) {
+                HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&d->h_err), sizeof(int),
+                                     hipHostMallocMapped | hipHostMallocCoherent));
+                *d->h_err = 0;
+            }
             d->d_err.ensure(1);
             HIPCHK(hipMemsetAsync(d->d_err.p, 0, sizeof(int), d->stream));
         }
@@ -793,10 +817,12 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             cc.st_s = d->debug ? d->d_st_s.p + (size_t)f0 * g.grid : nullptr;
             wc.dbg_v = d->debug ? d->d_dbg_v.p + (size_t)f0 * g.grid : nullptr;
             wc.row_visited = d->d_visited.p + (size_t)f0 * n_rows;
+            if (nc == 1) wc.rows = d->d_rows.p + n_rows;  // the one-frame order
             wc.entry = d->d_entry.p;
             d->err_word = (long long)(n_rows * std::min(chunk, n) * sc::kXcds);
             wc.fired = d->d_entry.p + d->err_word;  // per launch: zeroed with the entries
             wc.err = d->d_err.p;                    // sticky over launches and calls
+            HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&wc.err_host), d->h_err, 0));
             wc.int_ctl = wc.fired + 1;
             wc.spec = wc.int_ctl + 1 + std::min(chunk, n);
             d->spec_word = wc.spec - d->d_entry.p;
@@ -848,9 +874,15 @@ void check_chain(sc_detector *d) {
     if (!d->lazy || !d->chain_launched || !d->d_err.p) return;
     d->chain_launched = false;
     int err = 0;
-    HIPCHK(hipMemcpy(&err, d->d_err.p, sizeof(int), hipMemcpyDeviceToHost));
-    if (err) {
+    // the common case costs no device copy: the kernel raised the host flag
+    // with its first count (the stream has drained, so the flag is final)
+    if (*static_cast<volatile int *>(d->h_err)) {
+        HIPCHK(hipMemcpy(&err, d->d_err.p, sizeof(int), hipMemcpyDeviceToHost));
         HIPCHK(hipMemset(d->d_err.p, 0, sizeof(int)));
+        *d->h_err = 0;
+        if (!err) err = 1;
+    }
+    if (err) {
         throw Error{SC_ERR_DEVICE, "chain kernel: " + std::to_string(err) + " segment hand-off(s) timed out"};
     }
     if (d->d_prof.p) {
@@ -1357,6 +1389,28 @@ int sc_detector_wait_stream(sc_detector *d, void *stream) {
     });
 }
 
+int sc_detector_set_stream(sc_detector *d, void *stream, int use_own) {
+    return guarded([&] {
+        if (!d) throw Error{SC_ERR_INVALID, "null detector"};
+        HIPCHK(hipSetDevice(d->device));
+        hipStream_t s = use_own ? d->own_stream : static_cast<hipStream_t>(stream);
+        if (s == d->stream) return SC_OK;
+        if (s && !use_own) {
+            int dev = -1;
+            HIPCHK(hipStreamGetDevice(s, &dev));
+            if (dev != d->device)
+                throw Error{SC_ERR_INVALID, "stream of device " + std::to_string(dev) + ", detector on " +
+                                                std::to_string(d->device)};
+        }
+        hipEvent_t e = d->ev();
+        HIPCHK(hipEventRecord(e, d->stream));
+        HIPCHK(hipStreamWaitEvent(s, e, 0));
+        d->event_pool.push_back(e);
+        d->stream = s;
+        return SC_OK;
+    });
+}
+
 int sc_stream_wait_detector(sc_detector *d, void *stream) {
     return guarded([&] {
         if (!d) throw Error{SC_ERR_INVALID, "null detector"};
@@ -1541,8 +1595,8 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
             case SC_OPT_PHASES: o.phases = range(0, 2); break;
             case SC_OPT_SUBSTRIPS: o.substrips = range(0, 64); break;
             case SC_OPT_BAND_ROWS: o.band_rows = range(0, 64); break;
-            case SC_OPT_ROW_ORDER: o.row_order = range(0, 3); break;
-            case SC_OPT_ROW_BLOCK: o.row_block = range(1, 1 << 16); break;
+            case SC_OPT_ROW_ORDER: o.row_order = range(0, 3); o.order_set = true; break;
+            case SC_OPT_ROW_BLOCK: o.row_block = range(1, 1 << 16); o.order_set = true; break;
             case SC_OPT_CHAIN_CHUNK: o.chain_chunk = range(0, 1 << 20); regeo = false; break;
             case SC_OPT_LDS_WEIGHTS: o.lds_weights = range(-1, 1); regeo = false; break;
             case SC_OPT_WGS_PER_CU: o.wgs_per_cu = range(0, 4); regeo = false; break;

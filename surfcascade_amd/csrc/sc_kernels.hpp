@@ -178,6 +178,8 @@ struct WalkArgs {
     int row_max;     // chain kernel: most windows in one row segment (LDS sizing)
     int *entry;      // chain kernel: [frame*rows][kXcds] chain entry + 1 per segment (zeroed)
     int *err;        // chain kernel: hand-off timeouts, summed over launches and calls (must stay 0)
+    int *err_host;   // chain kernel: 1 once err is raised, in mapped host memory (sc_synchronize reads it
+                     // after the stream drains, with no device copy)
     int *fired;      // chain kernel: this launch's watchdog has fired (zeroed per launch)
     int *spec;       // chain kernel: speculative rounds of this launch (zeroed per launch)
     int drop_task1;  // test only: row task + 1 whose segment-0 hand-off is dropped (0: none)

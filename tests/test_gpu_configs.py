@@ -244,6 +244,51 @@ def test_stream_ordered_device_frames(sc, oracle, face_cascade):
         assert _det_set(got[got["frame"] == f]) == _det_set(ref)
 
 
+@pytest.mark.parametrize("which", ["default", "side"])
+def test_detector_on_torch_stream(sc, oracle, face_cascade, which):
+    """sc_detector_set_stream: the detector launches on torch's stream (the
+    null stream, or a side stream made current), so enqueue_device skips the
+    event pair; a slow torch producer before the scan and torch's read after
+    it are ordered by the stream alone.  Switching back to the detector's own
+    stream is ordered too."""
+    import torch
+    from surfcascade_amd.dist import merge_records
+    host = np.stack([_frame(1280, 720, 910 + k) for k in range(2)])
+    base = torch.from_numpy(host).to("cuda:0")
+    torch.cuda.synchronize()
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=8))
+    own = det.stream_ptr
+    side = torch.cuda.Stream(device="cuda:0") if which == "side" else torch.cuda.current_stream()
+    g = torch.Generator(device="cuda:0").manual_seed(2)
+    with torch.cuda.stream(side):
+        det.set_stream(side)
+        assert (det.stream_ptr or 0) == side.cuda_stream
+        recs = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda:0")
+        counts = torch.zeros(3, dtype=torch.int32, device="cuda:0")
+        for it in range(2):
+            m = torch.randn(2048, 2048, device="cuda:0", generator=g)
+            for _k in range(8):
+                m = (m @ m.T) / 2048.0
+            zero = (m[0, 0] * 0).nan_to_num(0.0).to(torch.int16)
+            frames = (base.to(torch.int16) + zero).to(torch.uint8)
+            det.enqueue_device(frames, recs, counts)
+            c_host = counts.clone().cpu().numpy()
+            r_host = recs.cpu().numpy()
+            del frames
+        det.synchronize()
+    det.set_stream(None)
+    assert det.stream_ptr == own
+    got = merge_records([c_host], [r_host], [0])
+    for f in range(2):
+        ref, _ = oracle.detect(oracle.integral(host[f]), face_cascade, oracle.Params(n_levels=8))
+        assert _det_set(got[got["frame"] == f]) == _det_set(ref)
+    # back on its own stream: the same frames, the same records
+    counts2 = torch.zeros(3, dtype=torch.int32, device="cuda:0")
+    det.enqueue_device(base, recs, counts2)
+    det.synchronize()
+    assert np.array_equal(counts2.cpu().numpy(), c_host)
+
+
 def test_device_entry_points_refuse_host_pointers(sc):
     """A host pointer (or another device's memory) where device memory is
     required is SC_ERR_INVALID, not a kernel fault."""

@@ -110,10 +110,12 @@ def test_grid_parity_kernel_paths(sc, oracle, face_cascade, chunk_min, substrips
         assert T.view(np.uint32).tobytes() == oracle.integral(img).view(np.uint32).tobytes()
 
 
-@pytest.mark.parametrize("order,block", [("0", None), ("1", None), ("2", "5")])
+@pytest.mark.parametrize("order,block", [("0", None), ("1", None), ("2", "5"), ("2", None), ("3", "5")])
 def test_chain_row_orders(sc, oracle, face_cascade, order, block):
-    """The chain kernel's task order (level-major, y-major, other row blocks
-    than the default 32) changes the schedule only, never the bits."""
+    """The chain kernel's task order (level-major, y-major, row blocks top-down
+    or bottom-up; one-frame launches deal the explicitly set order instead of
+    their default bottom-up blocks of 8) changes the schedule only, never the
+    bits."""
     opts = {"row_order": int(order)}
     if block:
         opts["row_block"] = int(block)
