@@ -156,6 +156,7 @@ struct sc_detector {
     PinnedBuf h_stage;           // host frames -> pinned -> d_frames (upload_frames)
     DevBuf<float4> d_table;
     DevBuf<uint32_t> d_carry;    // integral pass 1 -> pass 2: per-strip row prefixes
+    DevBuf<uint32_t> d_colblk;   // one-frame column pass: exact 32-row column sums (colseg)
     int table_frames = 0;
     DevBuf<sc_det_record> d_out;
     DevBuf<int> d_counters;
@@ -207,7 +208,7 @@ struct sc_detector {
         d_levels.release(); d_rows.release(); d_proj.release(); d_tasks.release();
         d_proj_all.release(); d_mine_cnt.release(); d_mine_off.release(); d_mine_win.release();
         d_feat.release();
-        d_frames.release(); d_table.release(); d_carry.release(); d_out.release(); d_counters.release();
+        d_frames.release(); d_table.release(); d_carry.release(); d_colblk.release(); d_out.release(); d_counters.release();
         d_visited.release(); d_queues.release(); d_entry.release(); d_err.release(); d_st_p.release(); d_st_s.release();
         d_dbg_v.release(); d_prof.release();
         h_stage.release();
@@ -719,6 +720,10 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     const bool two_pass_all = d->opt.integral_passes ? d->opt.integral_passes == 2 : n <= 3;
     const bool two_pass_pre = d->opt.integral_passes ? d->opt.integral_passes == 2 : pre <= 3;
     ra.rfull_n = fuse ? (two_pass_pre ? std::min(pre, n) : 0) : (two_pass_all ? n : 0);
+    if (n == 1 && two_pass_all && sc::colseg_segments() > 1) {
+        d->d_colblk.ensure((size_t)(g.H + 31) / 32 * g.tg.rowp * 4);
+        ra.colblk = d->d_colblk.p;
+    }
     hipEvent_t e0 = nullptr;
     timed_begin(d, &e0);
     const bool have_r = sc::launch_rowscan(ra, n, d->stream);

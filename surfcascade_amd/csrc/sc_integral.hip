@@ -456,7 +456,81 @@ __global__ __launch_bounds__(64) void colsum_plane_kernel(RowScanArgs a) {
     }
 }
 
+// One frame's column pass in parallel row segments (colblock + colseg).
+// colsum4's step S_{y+1} = S_y + (float)R_y is exact while the column's
+// running sum stays <= 2^24: the R_y are non-negative integers below 2^24,
+// so every partial sum up to that bound is an integer f32 holds exactly.  So
+// the wave of segment k ([ya, yb) of 1/SC_COLSEG of the height) starts a
+// column from the exact integer sum of the rows above ya (from exact 32-row
+// block sums) whenever that sum is <= 2^24.  A column whose sum passes 2^24
+// above yb continues in the same wave, step by step in order, down to row H;
+// the later segments leave it alone (each row is read and written by one
+// wave only: the pass is in place).  The same bits as the sequential walk for
+// every input; the walk is as long as the column's last exact segment start
+// allows (a 1080p bench frame passes 2^24 from row 939 on).
+#ifndef SC_COLSEG  // row segments (colsum4's one walk: 0.053 ms per 1080p frame; 4: 0.048, 8: 0.049, profiles/r4/colseg)
+#define SC_COLSEG 4
+#endif
+constexpr int kColBlk = 32;
+__global__ __launch_bounds__(64) void colblock_kernel(RowScanArgs a) {
+    const TableGeom g = a.g;
+    const int fi = blockIdx.x * 64 + threadIdx.x, blk = blockIdx.y;  // float within a table row
+    const int y0 = blk * kColBlk, y1 = min(g.H, y0 + kColBlk);
+    const long long rs = (long long)g.rowp * 4;
+    const uint32_t *rp = reinterpret_cast<const uint32_t *>(a.table + g.rowp) + fi;  // R_y at table row y+1
+    uint32_t s = 0u;  // (< 32 * 255 * W: exact; padding cells sum garbage nobody reads)
+#pragma unroll 8
+    for (int y = y0; y < y1; y++) s += rp[y * rs];
+    a.colblk[blk * rs + fi] = s;
+}
+
+__global__ __launch_bounds__(64) void colseg_kernel(RowScanArgs a, int seg_len) {
+    const TableGeom g = a.g;
+    const int lane = threadIdx.x, fi = blockIdx.x * 64 + lane;
+    const int H = g.H, ya = blockIdx.y * seg_len, yb = min(H, ya + seg_len);
+    const int f4 = fi >> 2, plane_cells = g.ph * g.Qp;
+    const int ci = g.cs == 2 ? f4 >> 1 : f4 % plane_cells;  // colsum_plane's cell -> column map
+    const int col = (ci % g.Qp) * g.ph + ci / g.Qp;
+    const bool live = col >= 1 && col <= g.W && ya < H;
+    float *cellp = reinterpret_cast<float *>(a.table + g.rowp) + fi;
+    const uint32_t *rp = reinterpret_cast<const uint32_t *>(cellp);
+    const long long rs = (long long)g.rowp * 4;
+    // exact sums above ya and above yb (yb < H: a multiple of kColBlk)
+    unsigned long long ea = 0ull, eb = 0ull;
+    if (live) {
+        for (int i = 0; i < ya / kColBlk; i++) ea += a.colblk[i * rs + fi];
+        eb = ea;
+        if (yb < H)
+            for (int i = ya / kColBlk; i < yb / kColBlk; i++) eb += a.colblk[i * rs + fi];
+    }
+    const bool act = live && ea <= (1ull << 24);            // this segment starts the column exactly
+    const int end = !act ? ya : (yb < H && eb <= (1ull << 24)) ? yb : H;  // else it walks on to H
+    int ye = end;  // the wave's last row (all lanes take part: no early exit above)
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) ye = max(ye, __shfl_xor(ye, o));
+    ye = __builtin_amdgcn_readfirstlane(ye);
+    if (!act) return;  // (no cross-lane work below)
+    float S = (float)(uint32_t)ea;  // exact
+    uint32_t ra[kSumAhead4];  // colsum4's walk over [ya, end)
+#pragma unroll
+    for (int k = 0; k < kSumAhead4; k++) ra[k] = rp[min(ya + k, end - 1) * rs];
+    for (int y0 = ya; y0 < ye; y0 += kSumAhead4) {
+        uint32_t rb[kSumAhead4];
+#pragma unroll
+        for (int k = 0; k < kSumAhead4; k++) rb[k] = rp[min(y0 + kSumAhead4 + k, end - 1) * rs];
+#pragma unroll
+        for (int k = 0; k < kSumAhead4; k++) {
+            S = S + (float)ra[k];
+            if (y0 + k < end) cellp[(y0 + k) * rs] = S;
+        }
+#pragma unroll
+        for (int k = 0; k < kSumAhead4; k++) ra[k] = rb[k];
+    }
+}
+
 }  // namespace
+
+int colseg_segments() { return SC_COLSEG; }
 
 #ifndef SC_RC_DWORD  // rowcarry4 (dword loads) when the rows start 4-B aligned
 #define SC_RC_DWORD 1
@@ -479,14 +553,22 @@ void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream
         if (!have_r)  // (rowcarry4 wrote the R rows already)
             hipLaunchKernelGGL(rowfull_kernel, dim3(ns64 * 2, a.g.H, n_frames), dim3(64), 0, s, a);
         // table order from 2 frames (C2's two prebuilt frames: 0.087 -> 0.062
-        // ms); one frame stays with colsum4 (0.054 vs 0.059 ms: its 240 walks
-        // are latency-bound, profiles/r3/g51)
-        if (SC_COLSUM_PLANE && n_frames >= 2)
+        // ms); one frame: colblock + colseg (0.048 ms), colsum4's one walk per
+        // column 0.053, colsum_plane 0.059 (profiles/r3/g51, r4/colseg)
+        if (SC_COLSUM_PLANE && n_frames >= 2) {
             hipLaunchKernelGGL(colsum_plane_kernel, dim3(a.g.rowp / 16, n_frames), dim3(64), 0, s, a);
-        else if (SC_COLSUM4)
+        } else if (SC_COLSEG > 1 && n_frames == 1 && a.colblk) {
+            const int seg = ((a.g.H + SC_COLSEG - 1) / SC_COLSEG + kColBlk - 1) / kColBlk * kColBlk;
+            const int nseg = (a.g.H + seg - 1) / seg;
+            // (block sums only above the last segment's start: nothing reads the rest)
+            if (nseg > 1)
+                hipLaunchKernelGGL(colblock_kernel, dim3(a.g.rowp / 16, (nseg - 1) * seg / kColBlk), dim3(64), 0, s, a);
+            hipLaunchKernelGGL(colseg_kernel, dim3(a.g.rowp / 16, nseg), dim3(64), 0, s, a, seg);
+        } else if (SC_COLSUM4) {
             hipLaunchKernelGGL(colsum4_kernel, dim3(ns64 * 8, n_frames), dim3(64), 0, s, a);
-        else
+        } else {
             hipLaunchKernelGGL(colsum_kernel, dim3(ns64 * 2, n_frames), dim3(64), 0, s, a);
+        }
     } else {
         hipLaunchKernelGGL(colstrip_kernel, dim3(ns64 * 2, n_frames), dim3(64), 0, s, a);
     }

@@ -115,6 +115,8 @@ struct RowScanArgs {
     long long zero_n[4];
     int rfull_n;  // rowcarry4: frames [0, rfull_n) also get their exact row prefixes R written
                   // into the table (the two-pass column pass's input; rowfull then skipped)
+    uint32_t *colblk;  // one-frame column pass in row segments (colseg): exact 32-row column
+                       // sums, [ceil(H/32)][rowp*4] (null: colsum4)
 };
 
 // Cascade kernel: persistent workgroups of 4 independent waves; a task is
@@ -247,6 +249,7 @@ void launch_features(const FeatureArgs &a, hipStream_t s);
 bool launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s);
 // two_pass: rowfull + colsum (small batches; rowfull skipped when have_r), else colstrip
 void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s, bool have_r = false);
+int colseg_segments();  // row segments of the one-frame column pass (0: colsum4)
 // Per-detector launch configuration: the device's CU count (queried once
 // per detector, no process-wide cache) and the SC_OPT_* launch options.
 struct LaunchCfg {

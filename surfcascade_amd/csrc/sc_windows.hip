@@ -1078,22 +1078,6 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             continue;
         }
         idle = 0;
-#if SC_PRIO_SEG  // A/B: one-frame issue priority by segment (1: segment 0 first, 2: the last segment first)
-        if (a.n_frames == 1) {
-            int lo = 3, hi = 0;
-#pragma unroll
-            for (int sl = 0; sl < kSlots; sl++)
-                if (st[sl] == 2) {
-                    lo = min(lo, tq[sl]);
-                    hi = max(hi, tq[sl]);
-                }
-            const int p = SC_PRIO_SEG == 1 ? 3 - lo : min(hi, 3);
-            if (p == 0) __builtin_amdgcn_s_setprio(0);
-            else if (p == 1) __builtin_amdgcn_s_setprio(1);
-            else if (p == 2) __builtin_amdgcn_s_setprio(2);
-            else __builtin_amdgcn_s_setprio(3);
-        }
-#endif
 
         // 2) one evaluation round over every active slot's next batch
 #if SC_ABL_EXTRA_RT  // timing ablation: SC_ABL_EXTRA_RT dependent round trips to L2 per round
