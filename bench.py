@@ -114,6 +114,8 @@ def parse():
                     help="steps of the batch-1 (single-frame) latency leg (0: skip)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="sc_detector_set_option (tuning / A-B runs; never changes results)")
+    ap.add_argument("--detector-stream", default="torch", choices=("torch", "own"),
+                    help="launch on torch's current stream (default) or the detector's own (events per call)")
     ap.add_argument("--stub", action="store_true",
                     help="test only: CPU stand-in detector + gloo (launcher test, not a measurement)")
     a = ap.parse_args()
@@ -362,7 +364,7 @@ def main():
         k, v = o.split("=", 1)
         opts[k] = int(v)
     det.set_options(**opts)
-    if not stub:  # launches on torch's current stream: stream-ordered with the bench's tensors, no event pair per call
+    if not stub and args.detector_stream == "torch":  # stream-ordered with the bench's tensors, no event pair per call
         det.set_stream(torch.cuda.current_stream(dev))
     if grid_shard:
         det.set_shard(rank, world)

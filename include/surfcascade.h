@@ -202,7 +202,8 @@ int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, 
                                 /* launch (12 or 16; 0: none yet)              */
 #define SC_INFO_COLUMN_PASS 8   /* the last call's integral column pass for the */
                                 /* frames built outside the chain kernel:      */
-                                /* 1 two-pass (rowcarry R + colsum), 2 colstrip */
+                                /* 1 two-pass (rowcarry R + colsum), 2 colstrip,*/
+                                /* 3 two-pass in row segments (one frame)      */
 #define SC_INFO_SPEC_ROUNDS 9   /* speculative evaluation rounds of the last    */
                                 /* chain launch (one-frame launches only)      */
 int sc_detector_info(sc_detector *d, int what, int64_t *value);

@@ -749,7 +749,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     } else {
         sc::launch_colscan(ra, n, two_pass_all, d->stream, have_r);
     }
-    d->last_colpass = (fuse ? two_pass_pre : two_pass_all) ? 1 : 2;
+    d->last_colpass = (fuse ? two_pass_pre : two_pass_all) ? (ra.colblk ? 3 : 1) : 2;
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_COLSCAN, e0);
 

@@ -555,6 +555,27 @@ def test_integral_extreme_content(sc, oracle, kind, passes):
     assert T.view(np.uint32).tobytes() == ref.view(np.uint32).tobytes()
 
 
+@pytest.mark.parametrize("W,H,amp", [(1920, 1080, 40), (1000, 517, 160)])
+def test_one_frame_column_pass_in_segments(sc, oracle, W, H, amp):
+    """One frame's column pass in row segments (colblock + colseg,
+    SC_INFO_COLUMN_PASS 3): period-4 stripes of amplitude `amp` make every
+    column's sum grow linearly, so the right-hand columns pass 2^24 inside a
+    middle segment (that segment walks them on to the bottom, the later ones
+    skip them) while the left-hand ones never do; the ragged height ends in a
+    short segment.  The table must still be the reference's, bit for bit."""
+    xx = np.mgrid[0:H, 0:W][1]
+    img = (((xx >> 1) & 1) * amp).astype(np.uint8)
+    ref = oracle.integral(img)
+    over = ref[1:] > 2 ** 24
+    first = np.where(over.any(axis=0), over.argmax(axis=0), H)
+    assert 0 < first.min() < H // 2 and (first == H).any()  # crossings mid-frame, and none
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1))
+    det.detect(img)
+    assert det.info("column_pass") == 3
+    T = det.dump_integral(W, H)
+    assert T.view(np.uint32).tobytes() == ref.view(np.uint32).tobytes()
+
+
 @pytest.mark.parametrize("layout", ["0", "1"])
 @pytest.mark.parametrize("W,H", [(1920, 1080), (257, 131)])
 def test_integral_fused_extreme_content(sc, oracle, layout, W, H):
