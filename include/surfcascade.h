@@ -246,11 +246,11 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
                               /* frame's table is <= 128 MiB and the launch    */
                               /* has 2+ frames), 12, 16                        */
 #define SC_OPT_INTEGRAL_FUSE 18 /* integral column walks inside the chain      */
-                              /* kernel: 0 auto (from 4 frames per launch, for */
-                              /* tables <= 128 MiB), 1 never, 2 whenever a     */
-                              /* launch has 2+ frames                          */
+                              /* kernel: 0 auto (from 4 frames per launch),   */
+                              /* 1 never, 2 whenever a launch has 2+ frames    */
 #define SC_OPT_INTEGRAL_PRE 19 /* fused: frames per launch integrated before   */
-                              /* the chain kernel (0: default 2)               */
+                              /* the chain kernel (0: default 2; 1 for tables  */
+                              /* > 128 MiB)                                    */
 #define SC_OPT_TEST_DROP_HANDOFF 20 /* test only (-1 off): the chain kernel drops */
                               /* the segment-0 hand-off of row task `value`  */
                               /* of every launch; the watchdog must then     */

@@ -682,21 +682,20 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
         }
     }
     // Fused integral (SC_OPT_INTEGRAL_FUSE): the first `pre` frames of every
-    // launch are integrated by their own kernels (2 by default: a frame's 60
-    // walks inside the chain kernel take longer than the chain takes over
-    // frame 0, 13.63 vs 13.74 ms chain kernel at C2, profiles/r3/g10), the
-    // column walks of the others run inside the chain kernel as a second
-    // task type, overlapping the gathers.  Auto: from
-    // 4 frames per launch, where colstrip would be the integral's column pass,
-    // and for tables that fit the Infinity Cache: a 4K frame's 265 MB table
-    // leaves it, its chain kernel already gathers from HBM beyond the
-    // fabric's rate and the walks' stores cost more than they hide (C4: 26.09
-    // vs 25.88 ms per 8-frame step, profiles/r3/g21).
-    const int pre = d->opt.integral_pre > 0 ? d->opt.integral_pre : 2;
+    // launch are integrated by their own kernels, the column walks of the
+    // others run inside the chain kernel as a second task type, overlapping
+    // the gathers.  Auto: from 4 frames per launch,
+    // where colstrip would be the integral's column pass.  `pre` is 2 for
+    // tables that fit the Infinity Cache (a frame's 60 walks inside the chain
+    // kernel take longer than the chain takes over frame 0: 13.63 vs 13.74 ms
+    // at C2, profiles/r3/g10) and 1 for larger ones (a 4K frame: C4 25.55 vs
+    // 25.77 ms per step unfused, 25.69 with 2, 25.82 with 3, profiles/r4/c4fuse;
+    // round 3's fused 4K kernel was slower than unfused, profiles/r3/g21).
+    const bool big_table = g.tg.frame4 * 16 > (128ll << 20);
+    const int pre = d->opt.integral_pre > 0 ? d->opt.integral_pre : big_table ? 1 : 2;
     const int fuse_from = d->opt.integral_fuse == 2 ? 2 : 4;
     const bool fuse = chain && d->opt.integral_fuse != 1 && std::min(chunk, n) >= fuse_from &&
-                      std::min(chunk, n) > pre &&
-                      (d->opt.integral_fuse == 2 || g.tg.frame4 * 16 <= (128ll << 20));
+                      std::min(chunk, n) > pre;
 
     sc::RowScanArgs ra{d_frames, (long long)H * stride, stride, d->d_table.p, g.tg, d->d_carry.p, {}, {}};
     // zeroed by rowcarry (stream order: before every kernel that uses them):

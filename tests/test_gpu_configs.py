@@ -111,8 +111,8 @@ def test_c5_bench_form_fused_12_waves(sc, oracle, ped_cascade):
 
 
 def test_c4_bench_form_colstrip_one_launch(sc, oracle, face_cascade):
-    """C4 as bench.py runs it, in small: several 4K frames x 32 levels in ONE
-    chain launch (12 waves, tables beyond the Infinity Cache, no fusion)
+    """C4's form below 4 frames per call: several 4K frames x 32 levels in
+    ONE chain launch (12 waves, tables beyond the Infinity Cache, no fusion)
     whose tables colstrip built.  Lowered thetas so every
     level reaches detections."""
     from surfcascade_amd import synth
@@ -124,6 +124,25 @@ def test_c4_bench_form_colstrip_one_launch(sc, oracle, face_cascade):
                                sc.ScanParams(n_levels=32), oracle.Params(n_levels=32), integral_passes=1)
     assert det.info("column_pass") == 2  # colstrip
     assert det.info("fused_frames") == 0
+    assert det.info("chain_waves") == 12
+    assert all(len(b) > 100 for b in batch)
+
+
+def test_c4_bench_form_fused_one_prebuilt(sc, oracle, face_cascade):
+    """C4 exactly as bench.py runs it, in small: 4K frames x 32 levels in one
+    12-wave chain launch whose first frame is integrated before it (two-pass;
+    one prebuilt frame since a 4K table is larger than 128 MiB) and whose
+    other frames' column walks run inside the chain kernel.  Lowered thetas
+    so every level reaches detections."""
+    from surfcascade_amd import synth
+    c = face_cascade
+    text = synth.write_cfg(synth.cascade_tree(c.n_weak, np.full(c.n_stages, 0.45, np.float32),
+                                              c.patch_index, c.w, c.bias))
+    frames = np.stack([_frame(3840, 2160, 4200 + k) for k in range(4)])
+    det, batch = _batch_parity(sc, oracle, oracle.cascade_from_cfg(text), sc.Model.parse(text), frames,
+                               sc.ScanParams(n_levels=32), oracle.Params(n_levels=32))
+    assert det.info("fused_frames") == 3
+    assert det.info("column_pass") == 1  # the prebuilt frame: rowcarry R rows + colsum
     assert det.info("chain_waves") == 12
     assert all(len(b) > 100 for b in batch)
 
