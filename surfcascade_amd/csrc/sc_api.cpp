@@ -196,7 +196,7 @@ struct sc_detector {
 
     ~sc_detector() {
         (void)hipSetDevice(device);
-        if (stream) (void)hipStreamSynchronize(stream);
+        (void)hipStreamSynchronize(stream);  // (also the null stream, sc_detector_set_stream(d, NULL, 0))
         if (own_stream && own_stream != stream) (void)hipStreamSynchronize(own_stream);
         for (auto &p : pending) {
             event_pool.push_back(p.a);
