@@ -2,7 +2,8 @@
 (RCCL), the same code path bench.py takes at N > 1 -- counts + capacities
 all_gather, the grow-and-rescan on overflow, the padded record all_gather --
 against sc_detect_batch of the same frames, and the stream-ordered
-StreamGather of bench.py's timed steps.  The multi-rank logic is covered
+StreamGather of bench.py's timed steps, with the detector on its own stream
+and on torch's (bench.py's form).  The multi-rank logic is covered
 by the gloo tests (tests/test_dist.py); N > 1 on GPUs runs in the driver's
 scaling bench.  Runs in a child process so the process group is torn down
 with it."""
@@ -35,6 +36,8 @@ text = synth.write_cfg(synth.cascade_tree(base.n_weak, np.full(base.n_stages, 0.
                                           base.patch_index, base.w, base.bias))
 frames = np.stack([synth.make_frame(640, 480, 70 + k) for k in range(3)])
 det = sc.Detector(sc.Model.parse(text), sc.ScanParams(n_levels=6))
+if STREAM == "torch":  # bench.py's form: the detector on torch's current stream
+    det.set_stream(torch.cuda.current_stream(0))
 dev = torch.from_numpy(frames).to("cuda:0")
 counts = torch.zeros(1 + len(frames), dtype=torch.int32, device="cuda:0")
 recs = torch.zeros(8 * sc.RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda:0")  # overflows
@@ -78,9 +81,10 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_rccl_one_rank_gather_equals_detect_batch(tmp_path):
+@pytest.mark.parametrize("stream", ["own", "torch"])
+def test_rccl_one_rank_gather_equals_detect_batch(tmp_path, stream):
     script = tmp_path / "rccl_gather.py"
-    script.write_text("ROOT = %r\nCFG = %r\n" % (ROOT, FACE_CFG) + SCRIPT)
+    script.write_text("ROOT = %r\nCFG = %r\nSTREAM = %r\n" % (ROOT, FACE_CFG, stream) + SCRIPT)
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, env=env,
