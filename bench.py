@@ -41,19 +41,30 @@ VALU_ISSUE_PEAK = 1024 * 0.5 * 2.4e9
 # 5a, calibrated against TD_TD_BUSY)
 TD_CYCLES_PER_LOAD = 16
 N_CUS = 256
-# the sources whose compiled code the PMC table (profiles/pmc_windows.json)
-# describes: an entry collected on other sources is stale and not reported
-KERNEL_SOURCES = ("sc_windows.hip", "sc_device.hpp", "sc_kernels.hpp", "sc_integral_dev.hpp", "sc_integral.hip")
+CSRC = os.path.join(ROOT, "surfcascade_amd", "csrc")
 
 
-def kernel_sources_sha():
-    """sha256 (16 hex) over the window / integral kernel sources."""
+def source_build_id(extra=""):
+    """The build id the Makefile gives a library built from the current tree
+    with EXTRA flags `extra` (sc_build_info "build_id"): sha256 over every
+    csrc/*.hip, *.hpp, *.cpp (sorted), the Makefile, include/surfcascade.h and
+    the flags string -- kernels, the launch schedule in sc_api.cpp and every
+    -D knob alike."""
     import hashlib
+    names = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp", ".cpp")))
     h = hashlib.sha256()
-    for f in KERNEL_SOURCES:
-        with open(os.path.join(ROOT, "surfcascade_amd", "csrc", f), "rb") as fh:
-            h.update(f.encode() + b"\0" + fh.read())
+    for path in [os.path.join(CSRC, f) for f in names] + [os.path.join(CSRC, "Makefile"),
+                                                            os.path.join(ROOT, "include", "surfcascade.h")]:
+        with open(path, "rb") as fh:
+            h.update(fh.read())
+    h.update(extra.encode())
     return h.hexdigest()[:16]
+
+
+def pmc_is_stale(pmc, build_id):
+    """A PMC entry describes the binary it was collected on: stale unless its
+    build id is the loaded library's."""
+    return bool(pmc) and pmc.get("build_id") != build_id
 
 
 MODELS = os.path.join(ROOT, "surfcascade_amd", "models")
@@ -480,9 +491,8 @@ def main():
         pipe_bytes = W * H + 64 * (W + 1) * (H + 1)
         pipe_s = max(sum(v[0] for v in kt.values()) / 1e3 / max(n_win, 1), 1e-12)
         pmc = pmc_for(args, B, W) if not opts and not stub else {}
-        src_sha = kernel_sources_sha()
-        pmc_stale = bool(pmc) and pmc.get("kernel_sources_sha") != src_sha
-        if pmc_stale:  # collected on other kernel sources: its counters describe another binary
+        binfo = {"build_id": None} if stub else sc.build_info()
+        if pmc_is_stale(pmc, binfo["build_id"]):  # collected on another build: its counters describe another binary
             pmc = {"source": pmc.get("source"), "stale": True}
         traffic, valu_insts = pmc.get("hbm_bytes_per_launch"), pmc.get("valu_insts_per_launch")
         line = {
@@ -511,7 +521,7 @@ def main():
             "roofline": roofline(achieved, traffic, valu_insts, avg_win_s, win_bytes, pipe_bytes * B,
                                  pipe_s, pmc, opts, fused),
             "kernel_ms_per_launch": {k: v[0] / max(v[1], 1) for k, v in kt.items()},
-            "kernel_sources_sha": src_sha,
+            "build": binfo,
             "visited_windows_last_step": visited,
             "detections_last_step": total_det,
         }
@@ -578,8 +588,8 @@ def roofline(achieved, traffic, valu_insts, avg_win_s, bytes_launch, pipe_bytes,
          "valu_insts_per_launch": valu_insts, "valu_peak_per_s": VALU_ISSUE_PEAK,
          "pmc_source": pmc.get("source")}
     if pmc.get("stale"):
-        r["pmc_stale"] = ("profiles/pmc_windows.json was collected on other kernel sources "
-                          "(kernel_sources_sha differs): traffic, valu, fabric and TD fields omitted")
+        r["pmc_stale"] = ("profiles/pmc_windows.json was collected on another build (its build_id is not "
+                          "the loaded library's): traffic, valu, fabric and TD fields omitted")
         return r
     c = pmc.get("counters_per_launch", {})
     # the level the kernel actually stresses: L2 misses (128-B lines from the

@@ -206,15 +206,19 @@ int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, 
                                 /* 3 two-pass in row segments (one frame)      */
 #define SC_INFO_SPEC_ROUNDS 9   /* speculative evaluation rounds of the last    */
                                 /* chain launch (one-frame launches only)      */
+#define SC_INFO_CHAIN_SUBQ 10   /* dequeue sub-queues per XCD of the last chain  */
+                                /* launch (4 one-frame launches, 1 batches)    */
+#define SC_INFO_TAIL_ROUNDS 11  /* drained-tail rounds of the last chain launch */
+                                /* (both parities of a lone task's batch)      */
 int sc_detector_info(sc_detector *d, int what, int64_t *value);
 
 /* ---- tuning and test options ---------------------------------------------
- * Options 1-14 and 17-19 are schedule / layout choices that never change a result bit
+ * Options 1-14, 17-19, 21 and 23 are schedule / layout choices that never change a result bit
  * (tests/test_gpu_parity.py runs each against the oracle); the defaults are
  * the measured-fastest.  Options 15-16 restrict the scan to a range of levels
  * (profiling of level groups): they DO change the result, to the windows of
- * those levels.  Option 20 is a test hook (a deliberately lost hand-off:
- * the call must fail, tests/test_gpu_parity.py).  The library reads no
+ * those levels.  Options 20 and 22 are test hooks (a deliberately lost
+ * hand-off or walk count: the call must fail, tests/test_gpu_configs.py).  The library reads no
  * environment variable: these are set per detector, explicitly. */
 #define SC_OPT_FULL_GRID 1    /* 1: evaluate every grid window (cascade + walk   */
                               /* kernels) instead of the lazy chain kernel (0) */
@@ -257,6 +261,18 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
                               /* raise SC_ERR_DEVICE at the next sync.  Only */
                               /* the test-hook build (lib/testhooks) accepts */
                               /* a value other than -1                       */
+#define SC_OPT_CHAIN_SUBQ 21  /* chain kernel dequeue counters per XCD queue: */
+                              /* 0 auto (4 for a one-frame launch, else 1),    */
+                              /* or 1..8                                       */
+#define SC_OPT_TEST_DROP_WALK 22 /* test only (-1 off): the fused column walk  */
+                              /* `value` of every launch does not count itself */
+                              /* done; tasks waiting for that frame's table    */
+                              /* must time out and the next sync raise         */
+                              /* SC_ERR_DEVICE (test-hook build only)          */
+#define SC_OPT_CHAIN_TAIL 23   /* chain kernel: once a wave finds every queue  */
+                              /* drained, its lone active task's rounds      */
+                              /* evaluate both parities: 0 auto (one-frame   */
+                              /* launches), 1 never, 2 always                */
 int sc_detector_set_option(sc_detector *d, int option, int64_t value);
 
 /* Enable per-window debug records (grid order) for the next detect calls. */
@@ -347,6 +363,14 @@ void sc_normalize_operand_range(int max_w, int max_h, double ss[2], double d[2])
 
 const char *sc_last_error(void);
 const char *sc_version(void);
+/* What this library was built from, as one JSON object: "build_id" (sha256
+ * prefix over every csrc/ source, this header, the Makefile and the extra
+ * -D flags), "flags" (those -D flags), "arch", and whether it is a timing
+ * "ablation" build (wrong results possible), a "test_hooks" build or a
+ * "profiling" build.  The product library reports flags "" and all three
+ * false (tests/test_abi.py).  No reference counterpart: measurement
+ * provenance (bench.py stamps its line and the PMC table with build_id). */
+const char *sc_build_info(void);
 
 #ifdef __cplusplus
 }

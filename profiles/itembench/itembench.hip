@@ -867,6 +867,120 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_dma(Args a) {
     }
 }
 
+// V16 (round 5): V15's LDS DMA, software-pipelined.
+// Each wave holds two 10-KiB slot sets (corner slots of half 0 and half 1 of
+// one 64-item chunk).  While chunk c runs Normalize + LR + the f64 sigmoid
+// (the item's long dependent VALU tail), the DMAs of BOTH halves of chunk
+// c+1 are in flight into the slots chunk c's box sums have just freed.  No
+// corner VGPRs are held across the tail (the register form spilled:
+// profiles/r3/pipe2), at the price of 20 KiB of LDS per wave: 6 waves per
+// CU next to the model.
+// The DMAs are issued as inline asm (global_load_lds_dwordx4, M0 = the slot's
+// LDS address): the compiler then inserts no "wait for every outstanding LDS
+// DMA" before each LDS read (the builtin made it wait vmcnt(0) before the LR
+// weight reads, which serialised the pipeline); its own waits for the
+// VMEM ops it knows stay conservative (the DMAs only add younger ops).
+// vmcnt bookkeeping (in-order vector-memory counter): at the top of chunk c
+// the outstanding VMEM ops are, oldest first, DMA(c).h0 [10], DMA(c).h1
+// [10], STORE(c-1) [1, not on a ticket's first chunk], ITEM(c+1) [1].
+// Same corners, same arithmetic: bit-exact with V0.
+__device__ __forceinline__ void dma16(unsigned lds, unsigned voff, const char *base) {
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+                 :: "s"(lds), "v"(voff), "s"(base) : "memory", "m0");
+}
+template <class P>
+__device__ __forceinline__ void dma_corners(const char *Tb, unsigned off, int half_off, const P &pj,
+                                            unsigned ldsA) {
+    int co[10];
+    corner_offsets(pj, co);
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++)
+#pragma unroll
+        for (int m = 0; m < 10; m++)
+            dma16(ldsA + (unsigned)(hh * 10 + m) * 1024u, off + ((unsigned)(hh * half_off + co[m]) << 4), Tb);
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_dmap(Args a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float4 *Wl; double *Bl; int4 *Rl; float *Sc;
+    stage<WAVES>(a, smem, Wl, Bl, Rl, Sc);
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float4 *slotA = reinterpret_cast<float4 *>(smem + (((size_t)a.K * (144 + 8 + 16) + a.n_levels * 4 + 63) & ~(size_t)63)) +
+                    (size_t)wv * 20 * 64;
+    const float4 *slotB = slotA + 10 * 64;
+    const unsigned ldsA = __builtin_amdgcn_readfirstlane(
+        (unsigned)(size_t)(__attribute__((address_space(3))) float4 *)slotA);
+    const int lane = threadIdx.x & 63;
+    const unsigned q0 = xcc();
+    const char *Tb = reinterpret_cast<const char *>(a.table);
+    for (unsigned qi = 0; qi < 8; qi++) {
+      const unsigned q = (q0 + qi) & 7;
+      const Item *I = a.items + q * a.cap;
+      float *O = a.out + q * a.cap;
+      const int n = a.n_items[q];
+      for (;;) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(&a.tickets[q * 64], 1);
+        b0 = __builtin_amdgcn_readfirstlane(b0) * kChunk * kBlock;
+        if (b0 >= n) break;
+        const int b1 = min(n, b0 + kChunk * kBlock);
+        auto item_at = [&](int c0) { const int i = c0 + lane; return I[i < b1 ? i : b0]; };
+        // prologue: chunk b0's corners in flight
+        Item it = item_at(b0);
+        InlinePatch pj = project(a, Rl, Sc, it);
+        dma_corners(Tb, it.origin << 4, a.g.hs, pj, ldsA);
+        for (int c = b0; c < b1; c += 64) {
+            const bool more = c + 64 < b1;
+            const Item itn = item_at(more ? c + 64 : c);  // ITEM(c+1): the youngest VMEM op
+            f2 h[2][8];
+            if (c == b0) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");  // DMA(c).h0 landed
+            else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            {
+                float4 cn[10];
+#pragma unroll
+                for (int m = 0; m < 10; m++) cn[m] = slotA[m * 64 + lane];
+                half_box(pj.shape, cn, h[0]);
+            }
+            if (c == b0) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");   // DMA(c).h1 landed
+            else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            {
+                float4 cn[10];
+#pragma unroll
+                for (int m = 0; m < 10; m++) cn[m] = slotB[m * 64 + lane];
+                half_box(pj.shape, cn, h[1]);
+            }
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // slots read; ITEM(c+1), STORE(c-1) done
+            {   // ITEM(c+1) consumed on every path: otherwise the compiler sees its
+                // load still pending past the branch and waits vmcnt(0) in the
+                // tail (which, unknown to it, would also wait for DMA(c+1))
+                const uint2 raw = __builtin_bit_cast(uint2, itn);
+                asm volatile("" :: "v"(raw.x), "v"(raw.y));
+            }
+            const int k = it.k;
+            if (more) {  // chunk c+1's corners into the freed slots
+                it = itn;
+                pj = project(a, Rl, Sc, it);
+                dma_corners(Tb, it.origin << 4, a.g.hs, pj, ldsA);
+            }
+            f2 fp[16];
+#pragma unroll
+            for (int cl = 0; cl < 4; cl++) {
+                fp[4 * cl] = h[0][2 * cl];
+                fp[4 * cl + 1] = h[0][2 * cl + 1];
+                fp[4 * cl + 2] = h[1][2 * cl];
+                fp[4 * cl + 3] = h[1][2 * cl + 1];
+            }
+            normalize2(fp);
+            const float o = lr_predict2(fp, Wl + k * 9, Bl[k]);
+            const int i = c + lane;
+            if (i < b1) O[i] = o;  // (lane 0 always stores: one VMEM op per chunk)
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+}
+
 }  // namespace
 
 extern "C" int ib_run(int variant, int waves, const Args *a, void *stream) {
@@ -877,7 +991,8 @@ extern "C" int ib_run(int variant, int waves, const Args *a, void *stream) {
     hipMemsetAsync(a->tickets, 0, 8 * 64 * 4, s);
 #define L(KER, WV) hipLaunchKernelGGL((KER<WV>), dim3(cus), dim3(WV * 64), lds, s, *a)
     if (variant == 0) {
-        if (waves == 8) L(k_base, 8); else if (waves == 12) L(k_base, 12); else if (waves == 16) L(k_base, 16); else return -1;
+        if (waves == 4) L(k_base, 4); else if (waves == 6) L(k_base, 6);
+        else if (waves == 8) L(k_base, 8); else if (waves == 12) L(k_base, 12); else if (waves == 16) L(k_base, 16); else return -1;
     } else if (variant == 1) {
         return -1;  // (V1, the software-pipelined item, retired: slower, profiles/r2/itembench.md)
     } else if (variant == 2) {
@@ -915,6 +1030,11 @@ extern "C" int ib_run(int variant, int waves, const Args *a, void *stream) {
         const size_t lt = ((lds + 63) & ~(size_t)63) + (size_t)waves * 10 * 1024;
         if (waves == 8) hipLaunchKernelGGL((k_dma<8>), dim3(cus), dim3(512), lt, s, *a);
         else if (waves == 12) hipLaunchKernelGGL((k_dma<12>), dim3(cus), dim3(768), lt, s, *a);
+        else return -1;
+    } else if (variant == 16) {  // pipelined LDS DMA: + 20 KiB per wave
+        const size_t lt = ((lds + 63) & ~(size_t)63) + (size_t)waves * 20 * 1024;
+        if (waves == 4) hipLaunchKernelGGL((k_dmap<4>), dim3(cus), dim3(256), lt, s, *a);
+        else if (waves == 6) hipLaunchKernelGGL((k_dmap<6>), dim3(cus), dim3(384), lt, s, *a);
         else return -1;
     } else if (variant == 3) {
         if (waves == 8) L(k_fold, 8); else if (waves == 12) L(k_fold, 12); else if (waves == 16) L(k_fold, 16); else return -1;

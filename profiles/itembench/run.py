@@ -214,7 +214,7 @@ def main():
         o = d_out.cpu().numpy().copy()
         if ref is None:
             ref = o
-        same = np.array_equal(o.view(np.uint32), ref.view(np.uint32)) if v in (0, 1, 3, 4, 8, 9, 10, 11, 12, 13, 15) else None
+        same = np.array_equal(o.view(np.uint32), ref.view(np.uint32)) if v in (0, 1, 3, 4, 8, 9, 10, 11, 12, 13, 15, 16) else None
         ts = []
         for _ in range(a.reps):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

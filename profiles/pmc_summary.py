@@ -41,20 +41,21 @@ def load(d):
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
-def sources_sha(d):
-    """kernel_sources_sha of the bench.py runs the passes profiled (their JSON
-    lines, profiles/collect_pmc_cfg.sh): one value, or an error."""
-    shas = set()
+def build_id(d):
+    """The library build id (sc_build_info) of the bench.py runs the passes
+    profiled (their JSON lines' "build", profiles/collect_pmc_cfg.sh): one
+    value, or an error."""
+    ids = set()
     for f in glob.glob(os.path.join(d, "*.json")):
         try:
             line = json.loads(open(f).read().strip().splitlines()[-1])
         except (ValueError, IndexError):
             continue
-        if "kernel_sources_sha" in line:
-            shas.add(line["kernel_sources_sha"])
-    if len(shas) != 1:
-        raise SystemExit("%s: expected one kernel_sources_sha over the passes, found %s" % (d, sorted(shas)))
-    return shas.pop()
+        if "build" in line:
+            ids.add(line["build"]["build_id"])
+    if len(ids) != 1:
+        raise SystemExit("%s: expected one build_id over the passes, found %s" % (d, sorted(ids)))
+    return ids.pop()
 
 
 # MI355X_MICROARCH.md (section "Indexed rows: gather into LDS"): 1,152-B rows
@@ -135,7 +136,7 @@ def main():
         for c, v in sorted(cs.items()):
             print("   %-36s %.6g" % (c, v))
         if k == "windows":
-            print("   kernel_sources_sha", sources_sha(a.dir))
+            print("   build_id", build_id(a.dir))
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
             hbm = (2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024
             print("   %-36s %.6g" % ("hbm_bytes_per_launch", hbm))
@@ -143,7 +144,7 @@ def main():
         cs = dict(res["windows"])
         ms = cs.pop("_dispatch_ms", None)
         out = {"config": a.config, "batch": a.batch, "width": a.width, "height": a.height, "levels": a.levels,
-               "source": a.dir, "kernel_sources_sha": sources_sha(a.dir), "counters_per_launch": cs,
+               "source": a.dir, "build_id": build_id(a.dir), "counters_per_launch": cs,
                "avg_launch_ms_pmc": ms,
                "hbm_bytes_per_launch": (2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024,
                "valu_insts_per_launch": cs.get("SQ_INSTS_VALU"),

@@ -4,7 +4,8 @@
 # Run on the GPU box from the repo root, e.g.
 #   gpurun -- 'bash profiles/run.sh r4x "pytest -k fused" "ab c2 3 old cur" "bench c4 --config C4"'
 # Outputs go to gpurun_out/<OUT>/.  Steps (one quoted string each):
-#   pytest [pytest args]          the GPU suite (-m gpu), or a -k / file subset
+#   pytest [pytest args]          the GPU suite (-m gpu), or a subset (PYTEST_K="a or b": a -k
+#                                 expression with spaces, which the step string cannot carry)
 #   smoke                         __graft_entry__.smoke()
 #   bench NAME [bench.py args]    one bench line -> NAME.json
 #   ab DIR ROUNDS V... [-- args]  interleaved A/B of library variants (profiles/build_variants.sh
@@ -26,7 +27,8 @@ step() {
   local kind=$1; shift
   case "$kind" in
     pytest)
-      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "$@" \
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        ${PYTEST_K:+-k "$PYTEST_K"} "$@" \
         > "$O/pytest.log" 2>&1; local rc=$?; tail -3 "$O/pytest.log"; return $rc ;;
     smoke)
       timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 && cat "$O/smoke.log" ;;

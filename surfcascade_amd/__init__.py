@@ -41,15 +41,17 @@ RECT_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("width", "<i4"), ("height", 
 
 KERNELS = ("rowscan", "colscan", "windows", "walk")
 
-# sc_detector_set_option keys (include/surfcascade.h SC_OPT_*): 1-14 and 17-19
-# are schedule and layout choices that never change a result bit; level_lo /
-# level_hi restrict the scan to the levels [lo, hi) (level-group profiling)
+# sc_detector_set_option keys (include/surfcascade.h SC_OPT_*): 1-14, 17-19
+# 21 and 23 are schedule and layout choices that never change a result bit;
+# level_lo / level_hi restrict the scan to the levels [lo, hi) (level-group
+# profiling); 20 and 22 are test hooks (test-hook build only)
 OPTIONS = {"full_grid": 1, "chunk_min": 2, "table_layout": 3, "phases": 4, "substrips": 5,
            "band_rows": 6, "row_order": 7, "row_block": 8, "chain_chunk": 9, "lds_weights": 10,
            "wgs_per_cu": 11, "profile": 12, "chain_segs": 13, "integral_passes": 14,
            "level_lo": 15, "level_hi": 16, "chain_waves": 17,
            "integral_fuse": 18, "integral_pre": 19,
-           "test_drop_handoff": 20}
+           "test_drop_handoff": 20, "chain_subq": 21, "test_drop_walk": 22,
+           "chain_tail": 23}
 
 # every symbol include/surfcascade.h declares
 EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_model_save",
@@ -61,7 +63,8 @@ EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_mode
            "sc_detector_set_shard", "sc_detector_set_option", "sc_detector_set_debug", "sc_debug_dump", "sc_set_timing", "sc_get_timing",
            "sc_group_rectangles", "sc_group_detections", "sc_fddb_format",
            "sc_miner_create", "sc_mine", "sc_mine_device", "sc_mine_batch", "sc_mine_batch_device", "sc_fast_nms", "sc_decode_jpeg_gray", "sc_imread_gray",
-           "sc_selftest_rn", "sc_normalize_operand_range", "sc_last_error", "sc_version")
+           "sc_selftest_rn", "sc_normalize_operand_range", "sc_last_error", "sc_version",
+           "sc_build_info")
 
 
 class SurfCascadeError(RuntimeError):
@@ -125,6 +128,7 @@ def load_library():
     P = ctypes.POINTER
     L.sc_last_error.restype = ctypes.c_char_p
     L.sc_version.restype = ctypes.c_char_p
+    L.sc_build_info.restype = ctypes.c_char_p
     L.sc_scan_params_default.argtypes = [P(ScanParams)]
     L.sc_model_load.argtypes = [ctypes.c_char_p, P(vp)]
     L.sc_model_parse.argtypes = [ctypes.c_char_p, sz, P(vp)]
@@ -172,6 +176,13 @@ def load_library():
     L.sc_normalize_operand_range.restype = None
     _lib = L
     return L
+
+
+def build_info():
+    """sc_build_info of the loaded library: {"build_id", "flags", "arch",
+    "ablation", "test_hooks", "profiling"} (include/surfcascade.h)."""
+    import json
+    return json.loads(load_library().sc_build_info().decode())
 
 
 def _check(rc):
@@ -407,6 +418,8 @@ class Model:
 class Detector:
     """Owns device model + buffers + one HIP stream (sc_detector)."""
 
+    _stream = None  # the stream object set_stream launches on (kept alive while in use)
+
     def __init__(self, cascade, params: ScanParams | None = None, device: int = 0):
         L = load_library()
         self.params = params or ScanParams()
@@ -424,6 +437,7 @@ class Detector:
         if self._h:
             load_library().sc_detector_destroy(self._h)
             self._h = None
+        self._stream = None
 
     def __del__(self):
         if getattr(self, "_h", None) and _lib is not None:
@@ -531,17 +545,23 @@ class Detector:
         """Launch on `stream` (a torch.cuda.Stream, or a raw hipStream_t of the
         detector's GPU, 0 = the null stream; None: the detector's own stream).
         On torch's current stream, enqueue_device needs no stream-order events
-        (sc_detector_set_stream)."""
+        (sc_detector_set_stream).  Lifetime: the detector keeps a reference to
+        the stream object until set_stream(None) or close(), because it
+        synchronises that stream when destroyed; a raw handle must stay valid
+        for as long itself (the caller owns it)."""
         if stream is None:
             _check(load_library().sc_detector_set_stream(self._h, None, 1))
+            self._stream = None
         else:
             ptr = int(getattr(stream, "cuda_stream", stream))
             _check(load_library().sc_detector_set_stream(self._h, ptr or None, 0))
+            self._stream = stream
 
     # -- introspection ---------------------------------------------------------
     def info(self, key):
         keys = {"levels": 1, "grid_windows": 2, "rows": 3, "table_pitch": 4, "visited": 5, "fused_frames": 6,
-                "chain_waves": 7, "column_pass": 8, "spec_rounds": 9}
+                "chain_waves": 7, "column_pass": 8, "spec_rounds": 9, "chain_subq": 10,
+                "tail_rounds": 11}
         v = ctypes.c_int64()
         _check(load_library().sc_detector_info(self._h, keys[key], ctypes.byref(v)))
         return v.value

@@ -135,6 +135,9 @@ struct sc_detector {
         int integral_fuse = 0;           // column walks inside the chain kernel: 0 auto, 1 never, 2 from 2 frames
         int integral_pre = 0;            // fused: frames integrated before the chain kernel (0: 2)
         int drop_handoff = -1;           // test only: task whose segment-0 hand-off is dropped (watchdog)
+        int drop_walk = -1;              // test only: fused column walk whose completion count is dropped
+        int chain_subq = 0;              // chain kernel dequeue sub-queues per XCD (0 auto: 4 one frame, else 1)
+        int chain_tail = 0;              // drained-tail both-parity rounds: 0 auto (one frame), 1 off, 2 on
     } opt;
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
@@ -182,6 +185,7 @@ struct sc_detector {
     int last_fused = 0;  // frames of the last call integrated inside the chain kernel
     int last_nseg = 8;   // segments per row of the last chain launch (profiling readout)
     int last_waves = 0;  // waves per workgroup of the last chain launch (SC_INFO_CHAIN_WAVES)
+    int last_subq = 0;   // dequeue sub-queues of the last chain launch (SC_INFO_CHAIN_SUBQ)
     int last_colpass = 0;  // column pass of the last call's prebuilt frames (SC_INFO_COLUMN_PASS)
     // timing
     bool timing = false;
@@ -668,7 +672,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     // watchdog-fired flag, the fused integral's walk counter and per-frame
     // walk counts (WalkArgs::int_ctl), the speculative-round count; sized
     // for the largest launch
-    auto entry_words = [&](int frames) { return (long long)n_rows * frames * sc::kXcds + 3 + frames; };
+    auto entry_words = [&](int frames) { return (long long)n_rows * frames * sc::kXcds + 4 + frames; };
     if (chain) {
         d->d_entry.ensure((size_t)entry_words(std::min(chunk, n)));
         if (!d->d_err.p) {
@@ -723,6 +727,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
         d->d_colblk.ensure((size_t)(g.H + 31) / 32 * g.tg.rowp * 4);
         ra.colblk = d->d_colblk.p;
     }
+    d->spec_word = -1;  // (set by a chain launch below: SC_INFO_SPEC_ROUNDS reads 0 otherwise)
     hipEvent_t e0 = nullptr;
     timed_begin(d, &e0);
     const bool have_r = sc::launch_rowscan(ra, n, d->stream);
@@ -843,6 +848,15 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             }
             wc.frame0 = f0;
             wc.drop_task1 = d->opt.drop_handoff + 1;  // SC_OPT_TEST_DROP_HANDOFF (0: none)
+            wc.drop_walk1 = d->opt.drop_walk + 1;     // SC_OPT_TEST_DROP_WALK (0: none)
+            // dequeue sub-queues (SC_OPT_CHAIN_SUBQ): 4 for a one-frame launch
+            // (chain kernel 0.589 vs 0.606 ms per 1080p frame), 1 for batches
+            // (C2 with 4: 17.0 vs 13.6 ms; profiles/r4/subq)
+            wc.subq = d->opt.chain_subq ? d->opt.chain_subq : (nc == 1 ? 4 : 1);
+            d->last_subq = wc.subq;
+            // drained-tail rounds on both parities (SC_OPT_CHAIN_TAIL): one-frame
+            // launches (the latency path) unless set
+            wc.tail_both = d->opt.chain_tail ? d->opt.chain_tail == 2 : nc == 1;
             wc.nseg = segs_for(nc);
             d->last_nseg = wc.nseg;
             wc.seg_shift = wc.nseg == 8 ? 0 : wc.nseg == 4 ? 1 : wc.nseg == 2 ? 2 : 3;
@@ -857,7 +871,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             }
             if (f0 > 0) {  // (the first chunk's were cleared by rowcarry)
                 HIPCHK(hipMemsetAsync(d->d_entry.p, 0, sizeof(int) * n_rows * nc * sc::kXcds, d->stream));
-                HIPCHK(hipMemsetAsync(wc.fired, 0, sizeof(int) * (size_t)(3 + std::min(chunk, n)), d->stream));  // + int_ctl, spec
+                HIPCHK(hipMemsetAsync(wc.fired, 0, sizeof(int) * (size_t)(4 + std::min(chunk, n)), d->stream));  // + int_ctl, spec[2]
                 HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kQueueWords, d->stream));
             }
             sc::launch_chain(cc, wc, launch_cfg(d), d->stream, &d->last_waves);
@@ -882,7 +896,9 @@ void check_chain(sc_detector *d) {
     // with its first count (the stream has drained, so the flag is final)
     if (*static_cast<volatile int *>(d->h_err)) {
         HIPCHK(hipMemcpy(&err, d->d_err.p, sizeof(int), hipMemcpyDeviceToHost));
-        HIPCHK(hipMemset(d->d_err.p, 0, sizeof(int)));
+        // (stream-ordered: the detector's stream is non-blocking, so a null-stream
+        // clear would not be ordered before the next call's kernels)
+        HIPCHK(hipMemsetAsync(d->d_err.p, 0, sizeof(int), d->stream));
         *d->h_err = 0;
         if (!err) err = 1;
     }
@@ -1538,14 +1554,17 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value) {
         case SC_INFO_TABLE_PITCH: *value = d->geo.tg.rowp; break;
         case SC_INFO_FUSED_FRAMES: *value = d->last_fused; break;
         case SC_INFO_CHAIN_WAVES: *value = d->last_waves; break;
+        case SC_INFO_CHAIN_SUBQ: *value = d->last_subq; break;
         case SC_INFO_COLUMN_PASS: *value = d->last_colpass; break;
-        case SC_INFO_SPEC_ROUNDS:  // the last chain launch's speculative rounds
+        case SC_INFO_SPEC_ROUNDS:  // the last chain launch's speculative / drained-tail rounds
+        case SC_INFO_TAIL_ROUNDS:
             return guarded([&] {
                 int v = 0;
                 if (d->spec_word >= 0) {
                     HIPCHK(hipSetDevice(d->device));
                     HIPCHK(hipStreamSynchronize(d->stream));
-                    HIPCHK(hipMemcpy(&v, d->d_entry.p + d->spec_word, sizeof(int), hipMemcpyDeviceToHost));
+                    HIPCHK(hipMemcpy(&v, d->d_entry.p + d->spec_word + (what == SC_INFO_TAIL_ROUNDS ? 1 : 0),
+                                     sizeof(int), hipMemcpyDeviceToHost));
                 }
                 *value = v;
                 return SC_OK;
@@ -1615,6 +1634,15 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
                 o.drop_handoff = range(-1, INT32_MAX - 1);
                 regeo = false;
                 break;
+            case SC_OPT_TEST_DROP_WALK:
+#if !defined(SC_TEST_HOOKS) || !SC_TEST_HOOKS
+                if (value != -1) throw Error{SC_ERR_INVALID, "test_drop_walk needs the test-hook build (lib/testhooks)"};
+#endif
+                o.drop_walk = range(-1, INT32_MAX - 1);
+                regeo = false;
+                break;
+            case SC_OPT_CHAIN_SUBQ: o.chain_subq = range(0, sc::kMaxSubQ); regeo = false; break;
+            case SC_OPT_CHAIN_TAIL: o.chain_tail = range(0, 2); regeo = false; break;
             case SC_OPT_CHAIN_WAVES:
                 o.chain_waves = range(0, 16);
                 if (o.chain_waves != 0 && o.chain_waves != 12 && o.chain_waves != 16)

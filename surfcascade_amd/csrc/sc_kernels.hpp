@@ -21,9 +21,20 @@
 
 #include "surfcascade.h"
 
+// Timing ablations (segments that start without their hand-off, walks that
+// store nothing, extra round trips / exp per item) give wrong results or
+// deliberately slow the kernels: a build that sets one must say it is an
+// ablation build, and then reports it (sc_build_info "ablation": true).
+#if !defined(SC_ABLATION_BUILD) &&                                                   \
+    ((defined(SC_ABL_NOWAIT) && SC_ABL_NOWAIT) || (defined(SC_ABL_EXTRA_RT) && SC_ABL_EXTRA_RT) || \
+     (defined(SC_ABL_EXTRA_EXP) && SC_ABL_EXTRA_EXP) || defined(SC_NO_WALK) ||                    \
+     (defined(SC_WALK_STORE) && SC_WALK_STORE == 0))
+#error "timing ablation flag set: build with -DSC_ABLATION_BUILD (never the product library)"
+#endif
+
 namespace sc {
 
-constexpr int kXcds = 8;          // MI355X: 8 XCDs, one L2 each
+constexpr int kXcds = 8;        // MI355X: 8 XCDs, one L2 each
 constexpr int kQueueStride = 64;  // ints between per-XCD queue words (own 256-B line each)
 constexpr int kMaxSubQ = 8;       // chain kernel: dequeue counters per XCD queue, at most
 constexpr int kQueueWords = kXcds * kMaxSubQ * kQueueStride;  // the queue buffer
@@ -183,11 +194,14 @@ struct WalkArgs {
     int *err_host;   // chain kernel: 1 once err is raised, in mapped host memory (sc_synchronize reads it
                      // after the stream drains, with no device copy)
     int *fired;      // chain kernel: this launch's watchdog has fired (zeroed per launch)
-    int *spec;       // chain kernel: speculative rounds of this launch (zeroed per launch)
+    int *spec;       // chain kernel: [0] speculative rounds, [1] drained-tail rounds of this launch (zeroed)
+    int tail_both;   // chain kernel: a drained wave's lone active task evaluates both parities per round
     int drop_task1;  // test only: row task + 1 whose segment-0 hand-off is dropped (0: none)
+    int drop_walk1;  // test only: fused column walk + 1 whose completion count is dropped (0: none)
     int frame0;      // chain kernel: first frame of this launch (record frame index)
     int nseg;        // chain kernel: segments per row (8; 4 for one-frame launches)
     int seg_shift;   // chain kernel: log2(kXcds / nseg)
+    int subq;        // chain kernel: dequeue counters per XCD queue (1..kMaxSubQ; 4 for one-frame launches)
     unsigned long long *prof;  // chain kernel, SC_PROF_CHAIN builds: phase cycle totals (or null)
     // Fused integral (chain kernel): colstrip's column walks of frames
     // [int_f0, n_frames) of this launch run inside the chain kernel as a

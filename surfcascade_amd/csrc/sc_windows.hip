@@ -629,12 +629,6 @@ __global__ __launch_bounds__(64) void walk_kernel(WalkArgs a) {
 #ifndef SC_ABL_EXTRA_RT
 #define SC_ABL_EXTRA_RT 0
 #endif
-#ifndef SC_SUBQ  // chain kernel: dequeue counters per XCD queue
-#define SC_SUBQ 1
-#endif
-constexpr int kSubQ = SC_SUBQ;
-static_assert(kSubQ >= 1 && kSubQ <= kMaxSubQ, "sub-queue count");
-
 #ifndef SC_CHAIN_SLOTS  // chain kernel: rows (tasks) a wave advances together
 #define SC_CHAIN_SLOTS 2
 #endif
@@ -745,6 +739,9 @@ __device__ __forceinline__ void fused_walk(const CascadeArgs &a, const WalkArgs 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
+#if SC_TEST_HOOKS  // test builds only: a lost walk count (the frame's readers must time out)
+    if (t + 1 == w.drop_walk1) return;
+#endif
     if (lead_lane()) __hip_atomic_fetch_add(&w.int_ctl[1 + f], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -810,13 +807,17 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     const int n_tasks = w.n_rows * a.n_frames;  // per segment queue, in row order
     const unsigned long long kEven = 0x5555555555555555ull;
     // queue of XCD q: segment q of every row, in row order, dealt through
-    // kSubQ counters on separate lines (sub-queue u: tasks u, u + kSubQ, ...;
-    // a few hundred waves per XCD dequeuing through one atomic word
-    // serialise on its line).  A drained sub-queue sends the wave on to the
-    // next one, then to the other XCDs' queues.
+    // nsq counters on separate lines (sub-queue u: tasks u, u + nsq, ...).
+    // A drained sub-queue sends the wave on to the next one, then to the
+    // other XCDs' queues.  nsq is per launch (WalkArgs::subq): one-frame
+    // launches use 4 (their ~400 waves per XCD otherwise serialise on one
+    // atomic word's line: chain kernel 0.589 vs 0.606 ms, profiles/r4/subq),
+    // batches 1 (sub-queues deal the row blocks out of order and cost their
+    // L2 locality: C2 +25 %)
     const int nsg = w.nseg, sh = w.seg_shift;  // segments per row; XCDs per segment = 1 << sh
+    const int nsq = w.subq;
     int q = (int)xcc_id(), empty = 0;
-    int u = (int)((blockIdx.x / kXcds * kChainWaves + wv) % kSubQ);
+    int u = (int)((blockIdx.x / kXcds * kChainWaves + wv) % nsq);
     bool drained = false;
     unsigned idle = 0;  // rounds with every task waiting for its entry
     unsigned long long idle_t0 = 0;  // when the current wait began (s_memrealtime)
@@ -878,6 +879,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     int frame[kSlots], level[kSlots], ys[kSlots];
     unsigned vtot = 0;  // windows this wave's chains visited (summed into row_visited at the end)
     unsigned nspec = 0;  // speculative rounds this wave ran (summed into *w.spec at the end)
+    unsigned ntail = 0;  // drained-tail both-parity rounds this wave ran (summed into w.spec[1])
 #pragma unroll
     for (int sl = 0; sl < kSlots; sl++) st[sl] = 0;  // 0 empty, 1 waiting for entry, 2 active, 3 waiting for the frame's table
 
@@ -899,8 +901,8 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             pre--;
             const int q0 = q & ((1 << sh) - 1);  // an XCD of segment 0
             int v = 0;
-            if (lead_lane()) v = atomicAdd(&a.queues[(q0 * kSubQ + u) * kQueueStride], 1);
-            v = ((__builtin_amdgcn_readfirstlane(v) * kSubQ + u) << sh) + q0;
+            if (lead_lane()) v = atomicAdd(&a.queues[(q0 * kMaxSubQ + u) * kQueueStride], 1);
+            v = ((__builtin_amdgcn_readfirstlane(v) * nsq + u) << sh) + q0;
             if (v < n_tasks) {
                 t = v;
                 qq = 0;
@@ -911,17 +913,17 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         }
         while (!drained) {
             int v = 0;
-            if (lead_lane()) v = atomicAdd(&a.queues[(q * kSubQ + u) * kQueueStride], 1);
-            v = ((__builtin_amdgcn_readfirstlane(v) * kSubQ + u) << sh) + (q & ((1 << sh) - 1));
+            if (lead_lane()) v = atomicAdd(&a.queues[(q * kMaxSubQ + u) * kQueueStride], 1);
+            v = ((__builtin_amdgcn_readfirstlane(v) * nsq + u) << sh) + (q & ((1 << sh) - 1));
             if (v < n_tasks) {
                 t = v;
                 qq = q >> sh;  // the segment
                 rd = row_desc(w.rows, v % w.n_rows);
                 return true;
             }
-            if (++empty == kXcds * kSubQ) {  // every sub-queue drained
+            if (++empty == kXcds * nsq) {  // every sub-queue drained
                 drained = true;
-            } else if (++u == kSubQ) {
+            } else if (++u == nsq) {
                 u = 0;
                 q = (q + 1) & (kXcds - 1);
             }
@@ -929,6 +931,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         return false;
     };
     int spec = -1;      // this round: speculative evaluation of waiting slot `spec` (both parities)
+    int tail = -1;      // this round: descriptor 1 evaluates the other parity of active slot `tail`'s batch
     unsigned spd = 0;   // bit sl: slot sl's task was evaluated speculatively
     // the chain leaves slot sl's segment at absolute position pos: hand it on
 #if SC_PROF_CHAIN  // task trace (profiling builds): realtime stamps per task at dequeue / start / finish
@@ -1027,6 +1030,16 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             SC_PROF(c_poll);
         }
         spec = -1;
+        tail = -1;
+        if (kSpec && w.tail_both && drained && n_active == 1) {
+            // the drained tail of a launch (no task left to dequeue anywhere):
+            // the lone active task's batch is evaluated on both parities at
+            // once, so a parity switch of its chain (after a good window)
+            // finds its windows evaluated instead of costing another
+            // stage-by-stage round; the launch's last tasks are its critical
+            // path and the CUs have idle issue slots then
+            tail = st[0] == 2 ? 0 : 1;
+        }
         if (n_active == 0 && kSpec && a.n_frames == 1) {  // (one-frame launches: latency-bound)
             // nothing to evaluate: the first waiting task not yet speculated
             // gets both parities of its first 2*kBatch windows evaluated now,
@@ -1049,30 +1062,33 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                 continue;
             }
             __builtin_amdgcn_s_sleep(4);
-            // a lost hand-off must not hang the GPU: after 0.5 s of waiting (the
-            // chip-wide 100 MHz clock) the waiting tasks start anyway, each
-            // counted in the sticky error word; once any wave's watchdog has
-            // fired in this launch (the per-launch flag), tasks waiting for
-            // an entry start at once (uncounted: the call raises already),
-            // while tasks waiting for their frame's table keep polling it
-            // (the walks always finish) unless their own wait timed out
+            // a lost hand-off or walk count must not hang the GPU: after 0.5 s
+            // of waiting (the chip-wide 100 MHz clock) the waiting tasks start
+            // anyway, each counted in the sticky error word; once any wave's
+            // watchdog has fired in this launch (the per-launch flag), every
+            // waiting task -- for an entry or for its frame's table -- starts
+            // at once, uncounted (the call raises already; its results are
+            // discarded), so a failed launch drains in about one timeout.
+            // The wait's clock restarts only when a slot did start.
             if (idle++ == 0) idle_t0 = __builtin_amdgcn_s_memrealtime();
             if ((idle & 255u) == 0u) {
                 int e = 0;
                 if (lead_lane()) e = __hip_atomic_load(w.fired, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const bool own = __builtin_amdgcn_s_memrealtime() - idle_t0 > 50000000ull;
                 if (__builtin_amdgcn_readfirstlane(e) != 0 || own) {
+                    bool started = false;
 #pragma unroll
                     for (int sl = 0; sl < kSlots; sl++)
-                        if (st[sl] == 1 || (own && st[sl] == 3)) {
+                        if (st[sl] == 1 || st[sl] == 3) {
                             if (own && lead_lane()) {
                                 atomicAdd(w.err, 1);
                                 __hip_atomic_store(w.err_host, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                                 __hip_atomic_store(w.fired, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             }
                             start(sl, j0[sl]);
+                            started = true;
                         }
-                    idle = 0;
+                    if (started) idle = 0;
                 }
             }
             continue;
@@ -1084,7 +1100,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
 #pragma unroll
         for (int i = 0; i < SC_ABL_EXTRA_RT; i++) {
             int v = 0;  // (word 1 of this XCD's queue line: unused, stays 0)
-            if (lead_lane()) v = atomicAdd(&a.queues[(q * kSubQ + u) * kQueueStride + 1], 0);
+            if (lead_lane()) v = atomicAdd(&a.queues[(q * kMaxSubQ + u) * kQueueStride + 1], 0);
             v = __builtin_amdgcn_readfirstlane(v);
             if (v == 0x7fffffff) drained = true;
         }
@@ -1092,14 +1108,19 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         // descriptor sl's task: slot sl's own, or in a speculative round the
         // waiting task `spec` at parity offset sl (selects, no dynamic index
         // into the per-slot registers)
-#define SC_OF(v, sl) (spec < 0 ? (v)[sl] : (spec == 0 ? (v)[0] : (v)[1]))
-#define SC_ACT(sl) (spec < 0 ? st[sl] == 2 : (sl) < 2)
+#define SC_OF(v, sl) (spec >= 0 ? (spec == 0 ? (v)[0] : (v)[1]) : tail >= 0 ? (tail == 0 ? (v)[0] : (v)[1]) : (v)[sl])
+#define SC_ACT(sl) (spec >= 0 || tail >= 0 ? (sl) < 2 : st[sl] == 2)
+        // the task whose bit arrays descriptor sl's windows belong to
+        const int own0 = spec >= 0 ? spec : tail >= 0 ? tail : 0, own1 = spec >= 0 ? spec : tail >= 0 ? tail : 1;
 #pragma unroll
         for (int sl = 0; sl < kSlots; sl++) {
             if (lead_lane()) {
                 SlotDesc dd{};
                 if (SC_ACT(sl)) {
-                    const int lv = SC_OF(level, sl), rr = spec < 0 ? r[sl] : sl, ns_ = SC_OF(nseg, sl);
+                    const int lv = SC_OF(level, sl), ns_ = SC_OF(nseg, sl);
+                    // speculative: both parities from the segment start; tail: the
+                    // chain's batch (from r) and the other parity's (from r + 1)
+                    const int rr = spec >= 0 ? sl : tail >= 0 ? SC_OF(r, sl) + sl : r[sl];
                     const LevelInfo &L = Lv[lv];
                     const int jb = SC_OF(j0, sl) + rr;  // the batch: jb, jb + 2, ...
                     dd.t_off = (unsigned)((long long)SC_OF(frame, sl) * g.frame4 + SC_OF(ys, sl) * g.rowp + g.win_cell(jb));
@@ -1121,7 +1142,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         auto need = [&](int slot) {  // window not evaluated yet (an earlier batch may have)
             const int sl = slot / kBatch, u = slot - sl * kBatch;
             const int k = desc[sl].r + 2 * u;
-            return ((evb(spec < 0 ? sl : spec)[k >> 6] >> (k & 63)) & 1ull) == 0ull;
+            return ((evb(sl == 0 ? own0 : own1)[k >> 6] >> (k & 63)) & 1ull) == 0ull;
         };
         // the windows this round evaluates, window c*64 + lane of each slot's batch
         unsigned long long mine[kSlots][kBatchChunks];
@@ -1140,7 +1161,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                 int *pk = park + sl * 10;
                 pk[0] = st[sl]; pk[1] = tq[sl]; pk[2] = tt[sl]; pk[3] = r[sl]; pk[4] = j0[sl];
                 pk[5] = nseg[sl]; pk[6] = frame[sl]; pk[7] = level[sl];
-                pk[8] = sl == 0 ? spec : (int)spd;
+                pk[8] = sl == 0 ? (spec >= 0 ? spec : tail >= 0 ? 2 + tail : -1) : (int)spd;
                 pk[9] = ys[sl];
             }
         }
@@ -1172,15 +1193,25 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             level[sl] = __builtin_amdgcn_readfirstlane(pk[7]);
             ys[sl] = __builtin_amdgcn_readfirstlane(pk[9]);
         }
-        spec = __builtin_amdgcn_readfirstlane(park[8]);
+        {
+            const int mode = __builtin_amdgcn_readfirstlane(park[8]);
+            spec = mode < 2 ? mode : -1;
+            tail = mode >= 2 ? mode - 2 : -1;
+        }
         spd = (unsigned)__builtin_amdgcn_readfirstlane(park[10 + 8]);
-        if (kSpec && spec >= 0) {  // a speculative round: results and bits into task `spec`'s arrays, no chain step
-            const int fr = spec == 0 ? frame[0] : frame[1], y = spec == 0 ? ys[0] : ys[1], jj = spec == 0 ? j0[0] : j0[1];
-            const LevelInfo &L = Lv[spec == 0 ? level[0] : level[1]];
+        if (kSpec && (spec >= 0 || tail >= 0)) {
+            // a speculative round: results and bits into task `spec`'s arrays,
+            // both parities from its segment start, no chain step; a tail
+            // round: both parities from slot `tail`'s chain position r, then
+            // its chain steps below
+            const int tg = spec >= 0 ? spec : tail;
+            const int fr = tg == 0 ? frame[0] : frame[1], y = tg == 0 ? ys[0] : ys[1], jj = tg == 0 ? j0[0] : j0[1];
+            const int r0 = spec >= 0 ? 0 : (tg == 0 ? r[0] : r[1]);
+            const LevelInfo &L = Lv[tg == 0 ? level[0] : level[1]];
             const long long gi0 = (long long)fr * w.grid_per_frame + L.grid_base +
                                   (long long)(y / w.step) * L.nx + jj;
-            unsigned long long *ev_ = evb(spec), *gd_ = gdb(spec), *dt_ = dtb(spec);
-            float *sg = s_seg(spec);
+            unsigned long long *ev_ = evb(tg), *gd_ = gdb(tg), *dt_ = dtb(tg);
+            float *sg = s_seg(tg);
 #pragma unroll
             for (int d = 0; d < 2; d++)
 #pragma unroll
@@ -1189,7 +1220,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     if (!mk) continue;
                     const bool in = (mk >> lane_id<RM>()) & 1ull;
                     const int u = c * 64 + lane_id<RM>();
-                    const int k = d + 2 * u;
+                    const int k = r0 + d + 2 * u;
                     bool good = false, det = false;
                     if (in) {
                         const int p = st_p[d * kBatch + u];
@@ -1207,18 +1238,21 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     }
                     const unsigned long long gm = __ballot(good), dm = __ballot(det);
                     if (lead_lane()) {
-                        const int base = d + 128 * c;
+                        const int base = r0 + d + 128 * c;
                         or_spread(ev_, base, mk);
                         if (gm) or_spread(gd_, base, gm);
                         if (dm) or_spread(dt_, base, dm);
                     }
                 }
             wave_sync();
-            SC_PROF(c_merge);
-            continue;
+            if (spec >= 0) {
+                SC_PROF(c_merge);
+                continue;
+            }
+            ntail++;
         }
 
-        // 3) per slot: merge the batch, advance the chain
+        // 3) per slot: merge the batch (a tail round's merged above), advance the chain
 #pragma unroll
         for (int sl = 0; sl < kSlots; sl++) {
             if (st[sl] != 2) continue;
@@ -1230,7 +1264,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             float *sg = s_seg(sl);
 #pragma unroll
             for (int c = 0; c < kBatchChunks; c++) {
-                const unsigned long long mk = mine[sl][c];
+                const unsigned long long mk = tail == sl ? 0ull : mine[sl][c];
                 if (!mk) continue;
                 const bool in = (mk >> lane_id<RM>()) & 1ull;
                 const int u = c * 64 + lane_id<RM>();
@@ -1330,6 +1364,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     if (vtot && lead_lane())
         atomicAdd(&w.row_visited[(blockIdx.x * kChainWaves + wv) % (w.n_rows * a.n_frames)], vtot);
     if (nspec && lead_lane()) atomicAdd(w.spec, (int)nspec);
+    if (ntail && lead_lane()) atomicAdd(w.spec + 1, (int)ntail);
 #undef SC_OF
 #undef SC_ACT
 #if SC_PROF_CHAIN

@@ -103,3 +103,53 @@ def test_option_keys_match_header():
     hdr = open(os.path.join(ROOT, "include", "surfcascade.h")).read()
     defs = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"#define SC_OPT_(\w+) (\d+)", hdr)}
     assert defs == sc.OPTIONS
+
+
+def test_product_library_build_info(sc):
+    """sc_build_info: the product library is no ablation, test-hook or
+    profiling build, was built with no extra -D knobs, and its build id is the
+    one the current sources give (bench.py stamps its line and checks the PMC
+    table against it: a schedule change in sc_api.cpp makes the PMC stale)."""
+    import importlib.util
+    info = sc.build_info()
+    assert info["arch"] == "gfx950"
+    assert info["flags"] == ""
+    assert info["ablation"] is False and info["test_hooks"] is False and info["profiling"] is False
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    assert info["build_id"] == b.source_build_id(), "library older than its sources: rebuild"
+    assert b.source_build_id("-DSC_TEST_HOOKS=1") != info["build_id"]
+
+
+def test_test_hook_library_says_so():
+    """The test-hook build (lib/testhooks) reports itself as one."""
+    import json
+    import subprocess
+    import sys
+    lib = os.path.join(ROOT, "surfcascade_amd", "lib", "testhooks", "libsurfcascade.so")
+    code = ("import ctypes,sys; L=ctypes.CDLL(sys.argv[1]); L.sc_build_info.restype=ctypes.c_char_p; "
+            "print(L.sc_build_info().decode())")
+    out = subprocess.run([sys.executable, "-c", "import torch; " + code, lib], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    info = json.loads(out.stdout.strip().splitlines()[-1])
+    assert info["test_hooks"] is True and info["ablation"] is False
+    assert info["flags"] == "-DSC_TEST_HOOKS=1"
+
+
+def test_ablation_flags_refuse_to_build(tmp_path):
+    """Every wrong-result timing ablation is an #error unless the build says
+    it is an ablation build (SC_ABLATION_BUILD)."""
+    import subprocess
+    csrc = os.path.join(ROOT, "surfcascade_amd", "csrc")
+    src = tmp_path / "probe.cpp"
+    src.write_text('#include "sc_kernels.hpp"\nint main() { return 0; }\n')
+    for flag in ("-DSC_ABL_NOWAIT=1", "-DSC_WALK_STORE=0", "-DSC_NO_WALK", "-DSC_ABL_EXTRA_RT=2",
+                 "-DSC_ABL_EXTRA_EXP=1"):
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-fsyntax-only", "-I" + csrc,
+               "-I" + os.path.join(ROOT, "include"), flag, str(src)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+        assert r.returncode != 0 and "timing ablation" in r.stderr, flag
+        r = subprocess.run(cmd + ["-DSC_ABLATION_BUILD"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, (flag, r.stderr[-1000:])

@@ -198,6 +198,166 @@ def test_watchdog_error_is_sticky_over_pipelined_steps(sc):
     assert "RAISED True" in r.stdout and "CLEAN AFTER" in r.stdout, r.stdout
 
 
+_WALK_CHILD = r"""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[1])
+import surfcascade_amd as sc
+from surfcascade_amd import synth
+host = np.stack([synth.make_frame(1280, 720, 720 + k) for k in range(5)])
+frames = torch.from_numpy(host).to("cuda:0")
+det = sc.Detector(sys.argv[2], sc.ScanParams(n_levels=6))
+recs = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda:0")
+counts = torch.zeros(6, dtype=torch.int32, device="cuda:0")
+det.enqueue_device(frames, recs, counts)
+det.synchronize()                              # clean, fused (frames 2-4 walked inside)
+print("FUSED", det.info("fused_frames"))
+det.set_option("test_drop_walk", 3)            # frame 2's 4th column walk never counts itself done
+det.enqueue_device(frames, recs, counts)
+det.set_option("test_drop_walk", -1)
+try:
+    det.synchronize()
+    print("NOT RAISED")
+except sc.SurfCascadeError as e:
+    print("RAISED", "hand-off" in str(e))
+det.enqueue_device(frames, recs, counts)
+det.synchronize()
+print("CLEAN AFTER")
+"""
+
+
+def test_watchdog_ends_a_lost_walk_count(sc):
+    """A fused column walk whose completion count is lost
+    (SC_OPT_TEST_DROP_WALK, test-hook build): the tasks waiting for that
+    frame's table must time out and the call raise SC_ERR_DEVICE, not spin
+    (after another wave's watchdog fired, the idle clock of a wave
+    waiting for a table kept restarting); the detector then works again."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=6))
+    with pytest.raises(sc.SurfCascadeError, match="test-hook build"):
+        det.set_option("test_drop_walk", 3)
+    lib = os.path.join(ROOT, "surfcascade_amd", "lib", "testhooks", "libsurfcascade.so")
+    env = dict(os.environ, SURFCASCADE_LIB=lib)
+    r = subprocess.run([sys.executable, "-c", _WALK_CHILD, ROOT, FACE_CFG], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "FUSED 3" in r.stdout, r.stdout
+    assert "RAISED True" in r.stdout and "CLEAN AFTER" in r.stdout, r.stdout
+
+
+def test_c2_bench_form_exact(sc, oracle, face_cascade):
+    """C2 exactly as bench.py measures it: 32 device-resident 1080p frames x
+    24 levels in ONE sc_enqueue_device call, the calibrated model
+    (models/face40_synth.cfg, not permissive thetas), the detector on torch's
+    stream; the launch must be the bench's (16 waves, 30 of 32 frames
+    integrated inside the chain kernel, one dequeue sub-queue).  Tables and
+    per-window stage / score bits of frames 0 (prebuilt), 2 and 31 (fused),
+    the visited set and the detections of every frame (VERDICT r4 next #2;
+    ObjDetector.cpp:188-212)."""
+    import torch
+    from surfcascade_amd import RECORD_DTYPE, synth
+    from surfcascade_amd.dist import merge_records
+    host = synth.make_frames(1920, 1080, 32, seed0=1000)  # bench.py's frames (seeds 1000..1031)
+    frames = torch.from_numpy(host).to("cuda:0")
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=24))
+    det.set_stream(torch.cuda.current_stream())
+    det.set_debug(True)
+    recs = torch.zeros((1 << 18) * RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda:0")
+    counts = torch.zeros(33, dtype=torch.int32, device="cuda:0")
+    det.enqueue_device(frames, recs, counts)
+    det.synchronize()
+    assert det.info("fused_frames") == 30
+    assert det.info("chain_waves") == 16
+    assert det.info("chain_subq") == 1
+    assert det.info("column_pass") == 1
+    got = merge_records([counts.cpu().numpy()], [recs.cpu().numpy()], [0])
+    params = oracle.Params(n_levels=24)
+    layout, _ = oracle.grid_layout(1920, 1080, params)
+    vis_all, det_all = 0, 0
+    for f in range(32):
+        T = oracle.integral(host[f])
+        if f in (0, 2, 31):
+            assert det.dump_integral(1920, 1080, frame=f).view(np.uint32).tobytes() == \
+                T.view(np.uint32).tobytes(), f
+        p, s, v = det.dump_grid(frame=f)
+        rp, rs = oracle.eval_grid(T, face_cascade, params)
+        if f in (0, 2, 31):
+            ev = p != -2
+            np.testing.assert_array_equal(p[ev], rp[ev])
+            assert s[ev].view(np.uint32).tobytes() == rs[ev].view(np.uint32).tobytes(), f
+        rv, _ = oracle.walk_grid(rp, rs, layout, face_cascade.n_stages, params.stride_score)
+        np.testing.assert_array_equal(v, rv)
+        ref, nv = oracle.detect(T, face_cascade, params)
+        assert nv == int(rv.sum())
+        mine = got[got["frame"] == f]
+        assert _det_set(mine) == _det_set(ref), f
+        vis_all += nv
+        det_all += len(ref)
+    assert det.info("visited") == vis_all
+    assert int(counts[0].item()) == det_all
+    det.set_stream(None)
+
+
+def test_one_frame_launch_uses_four_subqueues(sc, oracle, face_cascade):
+    """One-frame launches deal their tasks through 4 dequeue sub-queues per
+    XCD (SC_INFO_CHAIN_SUBQ), batches through one; results are the oracle's
+    at every sub-queue count (SC_OPT_CHAIN_SUBQ)."""
+    img = _frame(1920, 1080, 1234)
+    params = oracle.Params(n_levels=24)
+    T = oracle.integral(img)
+    ref, nv = oracle.detect(T, face_cascade, params)
+    rp, rs = oracle.eval_grid(T, face_cascade, params)
+    for q in (0, 1, 2, 3, 8):
+        det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=24)).set_options(chain_subq=q)
+        det.set_debug(True)
+        wins = det.detect(img)
+        assert det.info("chain_subq") == (4 if q == 0 else q)
+        p, s, _v = det.dump_grid()
+        ev = p != -2
+        np.testing.assert_array_equal(p[ev], rp[ev])
+        assert s[ev].view(np.uint32).tobytes() == rs[ev].view(np.uint32).tobytes()
+        assert det.info("visited") == nv
+        assert _det_set(wins) == _det_set(ref)
+
+
+@pytest.mark.parametrize("n_frames", [1, 5])
+def test_drained_tail_rounds_match(sc, oracle, face_cascade, n_frames):
+    """SC_OPT_CHAIN_TAIL: once a wave finds every queue drained, its lone
+    active task evaluates both parities per round.  Per-window bits, the
+    visited set and the detections are the oracle's with it forced on, off
+    and at the default (on for one-frame launches), for one frame and a
+    fused batch."""
+    frames = np.stack([_frame(1280, 720, 1300 + k) for k in range(n_frames)])
+    params = oracle.Params(n_levels=14)
+    layout, _ = oracle.grid_layout(1280, 720, params)
+    refs = []
+    for k in range(n_frames):
+        T = oracle.integral(frames[k])
+        rp, rs = oracle.eval_grid(T, face_cascade, params)
+        rv, _ = oracle.walk_grid(rp, rs, layout, face_cascade.n_stages, params.stride_score)
+        refs.append((rp, rs, rv, oracle.detect(T, face_cascade, params)[0]))
+    for mode in (0, 1, 2):
+        det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=14)).set_options(chain_tail=mode)
+        det.set_debug(True)
+        batch = det.detect_batch(frames)
+        tails = det.info("tail_rounds")
+        if mode == 1 or (mode == 0 and n_frames > 1):
+            assert tails == 0
+        else:
+            assert tails > 0
+        for k, (rp, rs, rv, ref) in enumerate(refs):
+            p, s_, v = det.dump_grid(frame=k)
+            ev = p != -2
+            np.testing.assert_array_equal(p[ev], rp[ev])
+            assert s_[ev].view(np.uint32).tobytes() == rs[ev].view(np.uint32).tobytes()
+            np.testing.assert_array_equal(v, rv)
+            assert _det_set(batch[k]) == _det_set(ref)
+
+
 def test_c3_rank_shard_32_frames_one_call(sc, oracle, face_cascade):
     """The C3 per-rank workload: 32 device-resident 1080p frames in ONE
     sc_enqueue_device call (bench.py --gpus 8 shards 256 frames this way);
