@@ -208,12 +208,10 @@ int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, 
                                 /* chain launch (one-frame launches only)      */
 #define SC_INFO_CHAIN_SUBQ 10   /* dequeue sub-queues per XCD of the last chain  */
                                 /* launch (4 one-frame launches, 1 batches)    */
-#define SC_INFO_TAIL_ROUNDS 11  /* drained-tail rounds of the last chain launch */
-                                /* (both parities of a lone task's batch)      */
 int sc_detector_info(sc_detector *d, int what, int64_t *value);
 
 /* ---- tuning and test options ---------------------------------------------
- * Options 1-14, 17-19, 21 and 23 are schedule / layout choices that never change a result bit
+ * Options 1-14, 17-19 and 21 are schedule / layout choices that never change a result bit
  * (tests/test_gpu_parity.py runs each against the oracle); the defaults are
  * the measured-fastest.  Options 15-16 restrict the scan to a range of levels
  * (profiling of level groups): they DO change the result, to the windows of
@@ -269,10 +267,6 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
                               /* done; tasks waiting for that frame's table    */
                               /* must time out and the next sync raise         */
                               /* SC_ERR_DEVICE (test-hook build only)          */
-#define SC_OPT_CHAIN_TAIL 23   /* chain kernel: once a wave finds every queue  */
-                              /* drained, its lone active task's rounds      */
-                              /* evaluate both parities: 0 auto (one-frame   */
-                              /* launches), 1 never, 2 always                */
 int sc_detector_set_option(sc_detector *d, int option, int64_t value);
 
 /* Enable per-window debug records (grid order) for the next detect calls. */

@@ -42,7 +42,7 @@ RECT_DTYPE = np.dtype([("x", "<i4"), ("y", "<i4"), ("width", "<i4"), ("height", 
 KERNELS = ("rowscan", "colscan", "windows", "walk")
 
 # sc_detector_set_option keys (include/surfcascade.h SC_OPT_*): 1-14, 17-19
-# 21 and 23 are schedule and layout choices that never change a result bit;
+# and 21 are schedule and layout choices that never change a result bit;
 # level_lo / level_hi restrict the scan to the levels [lo, hi) (level-group
 # profiling); 20 and 22 are test hooks (test-hook build only)
 OPTIONS = {"full_grid": 1, "chunk_min": 2, "table_layout": 3, "phases": 4, "substrips": 5,
@@ -50,8 +50,7 @@ OPTIONS = {"full_grid": 1, "chunk_min": 2, "table_layout": 3, "phases": 4, "subs
            "wgs_per_cu": 11, "profile": 12, "chain_segs": 13, "integral_passes": 14,
            "level_lo": 15, "level_hi": 16, "chain_waves": 17,
            "integral_fuse": 18, "integral_pre": 19,
-           "test_drop_handoff": 20, "chain_subq": 21, "test_drop_walk": 22,
-           "chain_tail": 23}
+           "test_drop_handoff": 20, "chain_subq": 21, "test_drop_walk": 22}
 
 # every symbol include/surfcascade.h declares
 EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_model_save",
@@ -560,8 +559,7 @@ class Detector:
     # -- introspection ---------------------------------------------------------
     def info(self, key):
         keys = {"levels": 1, "grid_windows": 2, "rows": 3, "table_pitch": 4, "visited": 5, "fused_frames": 6,
-                "chain_waves": 7, "column_pass": 8, "spec_rounds": 9, "chain_subq": 10,
-                "tail_rounds": 11}
+                "chain_waves": 7, "column_pass": 8, "spec_rounds": 9, "chain_subq": 10}
         v = ctypes.c_int64()
         _check(load_library().sc_detector_info(self._h, keys[key], ctypes.byref(v)))
         return v.value

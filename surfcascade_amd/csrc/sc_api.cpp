@@ -137,7 +137,6 @@ struct sc_detector {
         int drop_handoff = -1;           // test only: task whose segment-0 hand-off is dropped (watchdog)
         int drop_walk = -1;              // test only: fused column walk whose completion count is dropped
         int chain_subq = 0;              // chain kernel dequeue sub-queues per XCD (0 auto: 4 one frame, else 1)
-        int chain_tail = 0;              // drained-tail both-parity rounds: 0 auto (one frame), 1 off, 2 on
     } opt;
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
@@ -672,7 +671,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     // watchdog-fired flag, the fused integral's walk counter and per-frame
     // walk counts (WalkArgs::int_ctl), the speculative-round count; sized
     // for the largest launch
-    auto entry_words = [&](int frames) { return (long long)n_rows * frames * sc::kXcds + 4 + frames; };
+    auto entry_words = [&](int frames) { return (long long)n_rows * frames * sc::kXcds + 3 + frames; };
     if (chain) {
         d->d_entry.ensure((size_t)entry_words(std::min(chunk, n)));
         if (!d->d_err.p) {
@@ -854,9 +853,6 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             // (C2 with 4: 17.0 vs 13.6 ms; profiles/r4/subq)
             wc.subq = d->opt.chain_subq ? d->opt.chain_subq : (nc == 1 ? 4 : 1);
             d->last_subq = wc.subq;
-            // drained-tail rounds on both parities (SC_OPT_CHAIN_TAIL): one-frame
-            // launches (the latency path) unless set
-            wc.tail_both = d->opt.chain_tail ? d->opt.chain_tail == 2 : nc == 1;
             wc.nseg = segs_for(nc);
             d->last_nseg = wc.nseg;
             wc.seg_shift = wc.nseg == 8 ? 0 : wc.nseg == 4 ? 1 : wc.nseg == 2 ? 2 : 3;
@@ -871,7 +867,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             }
             if (f0 > 0) {  // (the first chunk's were cleared by rowcarry)
                 HIPCHK(hipMemsetAsync(d->d_entry.p, 0, sizeof(int) * n_rows * nc * sc::kXcds, d->stream));
-                HIPCHK(hipMemsetAsync(wc.fired, 0, sizeof(int) * (size_t)(4 + std::min(chunk, n)), d->stream));  // + int_ctl, spec[2]
+                HIPCHK(hipMemsetAsync(wc.fired, 0, sizeof(int) * (size_t)(3 + std::min(chunk, n)), d->stream));  // + int_ctl, spec
                 HIPCHK(hipMemsetAsync(d->d_queues.p, 0, sizeof(int) * sc::kQueueWords, d->stream));
             }
             sc::launch_chain(cc, wc, launch_cfg(d), d->stream, &d->last_waves);
@@ -1556,15 +1552,13 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value) {
         case SC_INFO_CHAIN_WAVES: *value = d->last_waves; break;
         case SC_INFO_CHAIN_SUBQ: *value = d->last_subq; break;
         case SC_INFO_COLUMN_PASS: *value = d->last_colpass; break;
-        case SC_INFO_SPEC_ROUNDS:  // the last chain launch's speculative / drained-tail rounds
-        case SC_INFO_TAIL_ROUNDS:
+        case SC_INFO_SPEC_ROUNDS:  // the last chain launch's speculative rounds
             return guarded([&] {
                 int v = 0;
                 if (d->spec_word >= 0) {
                     HIPCHK(hipSetDevice(d->device));
                     HIPCHK(hipStreamSynchronize(d->stream));
-                    HIPCHK(hipMemcpy(&v, d->d_entry.p + d->spec_word + (what == SC_INFO_TAIL_ROUNDS ? 1 : 0),
-                                     sizeof(int), hipMemcpyDeviceToHost));
+                    HIPCHK(hipMemcpy(&v, d->d_entry.p + d->spec_word, sizeof(int), hipMemcpyDeviceToHost));
                 }
                 *value = v;
                 return SC_OK;
@@ -1642,7 +1636,6 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
                 regeo = false;
                 break;
             case SC_OPT_CHAIN_SUBQ: o.chain_subq = range(0, sc::kMaxSubQ); regeo = false; break;
-            case SC_OPT_CHAIN_TAIL: o.chain_tail = range(0, 2); regeo = false; break;
             case SC_OPT_CHAIN_WAVES:
                 o.chain_waves = range(0, 16);
                 if (o.chain_waves != 0 && o.chain_waves != 12 && o.chain_waves != 16)

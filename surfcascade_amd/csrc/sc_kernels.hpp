@@ -194,8 +194,7 @@ struct WalkArgs {
     int *err_host;   // chain kernel: 1 once err is raised, in mapped host memory (sc_synchronize reads it
                      // after the stream drains, with no device copy)
     int *fired;      // chain kernel: this launch's watchdog has fired (zeroed per launch)
-    int *spec;       // chain kernel: [0] speculative rounds, [1] drained-tail rounds of this launch (zeroed)
-    int tail_both;   // chain kernel: a drained wave's lone active task evaluates both parities per round
+    int *spec;       // chain kernel: speculative rounds of this launch (zeroed per launch)
     int drop_task1;  // test only: row task + 1 whose segment-0 hand-off is dropped (0: none)
     int drop_walk1;  // test only: fused column walk + 1 whose completion count is dropped (0: none)
     int frame0;      // chain kernel: first frame of this launch (record frame index)

@@ -879,7 +879,6 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     int frame[kSlots], level[kSlots], ys[kSlots];
     unsigned vtot = 0;  // windows this wave's chains visited (summed into row_visited at the end)
     unsigned nspec = 0;  // speculative rounds this wave ran (summed into *w.spec at the end)
-    unsigned ntail = 0;  // drained-tail both-parity rounds this wave ran (summed into w.spec[1])
 #pragma unroll
     for (int sl = 0; sl < kSlots; sl++) st[sl] = 0;  // 0 empty, 1 waiting for entry, 2 active, 3 waiting for the frame's table
 
@@ -931,7 +930,6 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         return false;
     };
     int spec = -1;      // this round: speculative evaluation of waiting slot `spec` (both parities)
-    int tail = -1;      // this round: descriptor 1 evaluates the other parity of active slot `tail`'s batch
     unsigned spd = 0;   // bit sl: slot sl's task was evaluated speculatively
     // the chain leaves slot sl's segment at absolute position pos: hand it on
 #if SC_PROF_CHAIN  // task trace (profiling builds): realtime stamps per task at dequeue / start / finish
@@ -1030,16 +1028,6 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             SC_PROF(c_poll);
         }
         spec = -1;
-        tail = -1;
-        if (kSpec && w.tail_both && drained && n_active == 1) {
-            // the drained tail of a launch (no task left to dequeue anywhere):
-            // the lone active task's batch is evaluated on both parities at
-            // once, so a parity switch of its chain (after a good window)
-            // finds its windows evaluated instead of costing another
-            // stage-by-stage round; the launch's last tasks are its critical
-            // path and the CUs have idle issue slots then
-            tail = st[0] == 2 ? 0 : 1;
-        }
         if (n_active == 0 && kSpec && a.n_frames == 1) {  // (one-frame launches: latency-bound)
             // nothing to evaluate: the first waiting task not yet speculated
             // gets both parities of its first 2*kBatch windows evaluated now,
@@ -1108,19 +1096,14 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         // descriptor sl's task: slot sl's own, or in a speculative round the
         // waiting task `spec` at parity offset sl (selects, no dynamic index
         // into the per-slot registers)
-#define SC_OF(v, sl) (spec >= 0 ? (spec == 0 ? (v)[0] : (v)[1]) : tail >= 0 ? (tail == 0 ? (v)[0] : (v)[1]) : (v)[sl])
-#define SC_ACT(sl) (spec >= 0 || tail >= 0 ? (sl) < 2 : st[sl] == 2)
-        // the task whose bit arrays descriptor sl's windows belong to
-        const int own0 = spec >= 0 ? spec : tail >= 0 ? tail : 0, own1 = spec >= 0 ? spec : tail >= 0 ? tail : 1;
+#define SC_OF(v, sl) (spec < 0 ? (v)[sl] : (spec == 0 ? (v)[0] : (v)[1]))
+#define SC_ACT(sl) (spec < 0 ? st[sl] == 2 : (sl) < 2)
 #pragma unroll
         for (int sl = 0; sl < kSlots; sl++) {
             if (lead_lane()) {
                 SlotDesc dd{};
                 if (SC_ACT(sl)) {
-                    const int lv = SC_OF(level, sl), ns_ = SC_OF(nseg, sl);
-                    // speculative: both parities from the segment start; tail: the
-                    // chain's batch (from r) and the other parity's (from r + 1)
-                    const int rr = spec >= 0 ? sl : tail >= 0 ? SC_OF(r, sl) + sl : r[sl];
+                    const int lv = SC_OF(level, sl), rr = spec < 0 ? r[sl] : sl, ns_ = SC_OF(nseg, sl);
                     const LevelInfo &L = Lv[lv];
                     const int jb = SC_OF(j0, sl) + rr;  // the batch: jb, jb + 2, ...
                     dd.t_off = (unsigned)((long long)SC_OF(frame, sl) * g.frame4 + SC_OF(ys, sl) * g.rowp + g.win_cell(jb));
@@ -1142,7 +1125,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         auto need = [&](int slot) {  // window not evaluated yet (an earlier batch may have)
             const int sl = slot / kBatch, u = slot - sl * kBatch;
             const int k = desc[sl].r + 2 * u;
-            return ((evb(sl == 0 ? own0 : own1)[k >> 6] >> (k & 63)) & 1ull) == 0ull;
+            return ((evb(spec < 0 ? sl : spec)[k >> 6] >> (k & 63)) & 1ull) == 0ull;
         };
         // the windows this round evaluates, window c*64 + lane of each slot's batch
         unsigned long long mine[kSlots][kBatchChunks];
@@ -1161,7 +1144,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                 int *pk = park + sl * 10;
                 pk[0] = st[sl]; pk[1] = tq[sl]; pk[2] = tt[sl]; pk[3] = r[sl]; pk[4] = j0[sl];
                 pk[5] = nseg[sl]; pk[6] = frame[sl]; pk[7] = level[sl];
-                pk[8] = sl == 0 ? (spec >= 0 ? spec : tail >= 0 ? 2 + tail : -1) : (int)spd;
+                pk[8] = sl == 0 ? spec : (int)spd;
                 pk[9] = ys[sl];
             }
         }
@@ -1193,25 +1176,15 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             level[sl] = __builtin_amdgcn_readfirstlane(pk[7]);
             ys[sl] = __builtin_amdgcn_readfirstlane(pk[9]);
         }
-        {
-            const int mode = __builtin_amdgcn_readfirstlane(park[8]);
-            spec = mode < 2 ? mode : -1;
-            tail = mode >= 2 ? mode - 2 : -1;
-        }
+        spec = __builtin_amdgcn_readfirstlane(park[8]);
         spd = (unsigned)__builtin_amdgcn_readfirstlane(park[10 + 8]);
-        if (kSpec && (spec >= 0 || tail >= 0)) {
-            // a speculative round: results and bits into task `spec`'s arrays,
-            // both parities from its segment start, no chain step; a tail
-            // round: both parities from slot `tail`'s chain position r, then
-            // its chain steps below
-            const int tg = spec >= 0 ? spec : tail;
-            const int fr = tg == 0 ? frame[0] : frame[1], y = tg == 0 ? ys[0] : ys[1], jj = tg == 0 ? j0[0] : j0[1];
-            const int r0 = spec >= 0 ? 0 : (tg == 0 ? r[0] : r[1]);
-            const LevelInfo &L = Lv[tg == 0 ? level[0] : level[1]];
+        if (kSpec && spec >= 0) {  // a speculative round: results and bits into task `spec`'s arrays, no chain step
+            const int fr = spec == 0 ? frame[0] : frame[1], y = spec == 0 ? ys[0] : ys[1], jj = spec == 0 ? j0[0] : j0[1];
+            const LevelInfo &L = Lv[spec == 0 ? level[0] : level[1]];
             const long long gi0 = (long long)fr * w.grid_per_frame + L.grid_base +
                                   (long long)(y / w.step) * L.nx + jj;
-            unsigned long long *ev_ = evb(tg), *gd_ = gdb(tg), *dt_ = dtb(tg);
-            float *sg = s_seg(tg);
+            unsigned long long *ev_ = evb(spec), *gd_ = gdb(spec), *dt_ = dtb(spec);
+            float *sg = s_seg(spec);
 #pragma unroll
             for (int d = 0; d < 2; d++)
 #pragma unroll
@@ -1220,7 +1193,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     if (!mk) continue;
                     const bool in = (mk >> lane_id<RM>()) & 1ull;
                     const int u = c * 64 + lane_id<RM>();
-                    const int k = r0 + d + 2 * u;
+                    const int k = d + 2 * u;
                     bool good = false, det = false;
                     if (in) {
                         const int p = st_p[d * kBatch + u];
@@ -1238,21 +1211,18 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     }
                     const unsigned long long gm = __ballot(good), dm = __ballot(det);
                     if (lead_lane()) {
-                        const int base = r0 + d + 128 * c;
+                        const int base = d + 128 * c;
                         or_spread(ev_, base, mk);
                         if (gm) or_spread(gd_, base, gm);
                         if (dm) or_spread(dt_, base, dm);
                     }
                 }
             wave_sync();
-            if (spec >= 0) {
-                SC_PROF(c_merge);
-                continue;
-            }
-            ntail++;
+            SC_PROF(c_merge);
+            continue;
         }
 
-        // 3) per slot: merge the batch (a tail round's merged above), advance the chain
+        // 3) per slot: merge the batch, advance the chain
 #pragma unroll
         for (int sl = 0; sl < kSlots; sl++) {
             if (st[sl] != 2) continue;
@@ -1264,7 +1234,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             float *sg = s_seg(sl);
 #pragma unroll
             for (int c = 0; c < kBatchChunks; c++) {
-                const unsigned long long mk = tail == sl ? 0ull : mine[sl][c];
+                const unsigned long long mk = mine[sl][c];
                 if (!mk) continue;
                 const bool in = (mk >> lane_id<RM>()) & 1ull;
                 const int u = c * 64 + lane_id<RM>();
@@ -1364,7 +1334,6 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     if (vtot && lead_lane())
         atomicAdd(&w.row_visited[(blockIdx.x * kChainWaves + wv) % (w.n_rows * a.n_frames)], vtot);
     if (nspec && lead_lane()) atomicAdd(w.spec, (int)nspec);
-    if (ntail && lead_lane()) atomicAdd(w.spec + 1, (int)ntail);
 #undef SC_OF
 #undef SC_ACT
 #if SC_PROF_CHAIN

@@ -324,40 +324,6 @@ def test_one_frame_launch_uses_four_subqueues(sc, oracle, face_cascade):
         assert _det_set(wins) == _det_set(ref)
 
 
-@pytest.mark.parametrize("n_frames", [1, 5])
-def test_drained_tail_rounds_match(sc, oracle, face_cascade, n_frames):
-    """SC_OPT_CHAIN_TAIL: once a wave finds every queue drained, its lone
-    active task evaluates both parities per round.  Per-window bits, the
-    visited set and the detections are the oracle's with it forced on, off
-    and at the default (on for one-frame launches), for one frame and a
-    fused batch."""
-    frames = np.stack([_frame(1280, 720, 1300 + k) for k in range(n_frames)])
-    params = oracle.Params(n_levels=14)
-    layout, _ = oracle.grid_layout(1280, 720, params)
-    refs = []
-    for k in range(n_frames):
-        T = oracle.integral(frames[k])
-        rp, rs = oracle.eval_grid(T, face_cascade, params)
-        rv, _ = oracle.walk_grid(rp, rs, layout, face_cascade.n_stages, params.stride_score)
-        refs.append((rp, rs, rv, oracle.detect(T, face_cascade, params)[0]))
-    for mode in (0, 1, 2):
-        det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=14)).set_options(chain_tail=mode)
-        det.set_debug(True)
-        batch = det.detect_batch(frames)
-        tails = det.info("tail_rounds")
-        if mode == 1 or (mode == 0 and n_frames > 1):
-            assert tails == 0
-        else:
-            assert tails > 0
-        for k, (rp, rs, rv, ref) in enumerate(refs):
-            p, s_, v = det.dump_grid(frame=k)
-            ev = p != -2
-            np.testing.assert_array_equal(p[ev], rp[ev])
-            assert s_[ev].view(np.uint32).tobytes() == rs[ev].view(np.uint32).tobytes()
-            np.testing.assert_array_equal(v, rv)
-            assert _det_set(batch[k]) == _det_set(ref)
-
-
 def test_c3_rank_shard_32_frames_one_call(sc, oracle, face_cascade):
     """The C3 per-rank workload: 32 device-resident 1080p frames in ONE
     sc_enqueue_device call (bench.py --gpus 8 shards 256 frames this way);
