@@ -25,7 +25,11 @@ def load(d):
     also hold launches of another shape (a batch-1 leg, a chunk tail): only
     dispatches lasting at least half the kernel's longest in that pass count."""
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
-    for f in glob.glob(os.path.join(d, "*", "pmc_counter_collection.csv")):
+    # rocprofv3 output dirs (PASS/pmc_counter_collection.csv), or the committed
+    # copies of their counter files (PASS.csv)
+    files = glob.glob(os.path.join(d, "*", "pmc_counter_collection.csv")) or \
+        [f for f in glob.glob(os.path.join(d, "*.csv")) if "Counter_Name" in open(f).readline()]
+    for f in files:
         rows = []
         for row in csv.DictReader(open(f)):
             name = next((v for k, v in KERNELS.items() if k in row["Kernel_Name"]), None)

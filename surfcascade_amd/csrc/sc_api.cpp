@@ -447,11 +447,12 @@ void build_geometry(sc_detector *d, int W, int H) {
         // rows that fits its L2: 14 % less kernel time than plain level-major
         // order (0) on the C2 frames; blocks of 64 rows 1 % and of 128 rows
         // 3 % slower than 32 (profiles/r1/sweep); 1: y-major.
-        // One-frame launches deal a second list (rows1): blocks of 8 grid rows
+        // One-frame launches deal a second list (rows1): blocks of 4 grid rows
         // bottom-up (3), so the last block dealt holds every level's top rows
         // and the wide levels' short rows end the launch: chain kernel 0.606
-        // vs 0.614 ms (profiles/r4/order/); SC_OPT_ROW_ORDER / _ROW_BLOCK set
-        // explicitly apply to both lists.
+        // vs 0.614 ms with blocks of 8 (profiles/r4/order/), 0.5822 vs 0.5854
+        // with 4 (4 sub-queues, profiles/r5/e); SC_OPT_ROW_ORDER / _ROW_BLOCK
+        // set explicitly apply to both lists.
         // (The full-grid tasks above are built from the level-major list.)
         auto order = [&](std::vector<int2> rows, int mode, int blk) {
             if (mode == 1)
@@ -466,7 +467,7 @@ void build_geometry(sc_detector *d, int W, int H) {
             return rows;
         };
         ng.rows1 = d->opt.order_set ? order(ng.rows, d->opt.row_order, d->opt.row_block * ng.step)
-                                    : order(ng.rows, 3, 8 * ng.step);
+                                    : order(ng.rows, 3, 4 * ng.step);
         ng.rows = order(ng.rows, d->opt.row_order, d->opt.row_block * ng.step);
     }
     d->d_tasks.ensure(std::max<size_t>(ng.tasks.size(), 1));
@@ -729,7 +730,8 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     d->spec_word = -1;  // (set by a chain launch below: SC_INFO_SPEC_ROUNDS reads 0 otherwise)
     hipEvent_t e0 = nullptr;
     timed_begin(d, &e0);
-    const bool have_r = sc::launch_rowscan(ra, n, d->stream);
+    bool colblk_done = false;
+    const bool have_r = sc::launch_rowscan(ra, n, d->stream, &colblk_done);
     HIPCHK(hipGetLastError());
     timed_end(d, SC_KERNEL_ROWSCAN, e0);
 
@@ -750,7 +752,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             sc::launch_colscan(rc, std::min(pre, n - f0), two_pass_pre, d->stream, have_r && f0 == 0);
         }
     } else {
-        sc::launch_colscan(ra, n, two_pass_all, d->stream, have_r);
+        sc::launch_colscan(ra, n, two_pass_all, d->stream, have_r, colblk_done);
     }
     d->last_colpass = (fuse ? two_pass_pre : two_pass_all) ? (ra.colblk ? 3 : 1) : 2;
     HIPCHK(hipGetLastError());
@@ -1638,8 +1640,8 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
             case SC_OPT_CHAIN_SUBQ: o.chain_subq = range(0, sc::kMaxSubQ); regeo = false; break;
             case SC_OPT_CHAIN_WAVES:
                 o.chain_waves = range(0, 16);
-                if (o.chain_waves != 0 && o.chain_waves != 12 && o.chain_waves != 16)
-                    throw Error{SC_ERR_INVALID, "chain_waves: 0, 12 or 16"};
+                if (o.chain_waves != 0 && o.chain_waves != 8 && o.chain_waves != 12 && o.chain_waves != 16)
+                    throw Error{SC_ERR_INVALID, "chain_waves: 0, 8, 12 or 16"};
                 regeo = false;
                 break;
             case SC_OPT_LEVEL_LO: o.level_lo = range(0, 256); break;

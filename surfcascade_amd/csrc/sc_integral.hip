@@ -40,6 +40,8 @@ constexpr int kColUnroll = SC_COL_UNROLL;  // rows per colstrip block (two block
 #define SC_COL_WAVES 1
 #endif
 
+constexpr int kColBlk = 32;  // one-frame column pass: rows per exact column-block sum (colseg)
+
 #ifndef SC_RC_ROWS  // rowcarry: rows (waves) per workgroup
 #define SC_RC_ROWS 1
 #endif
@@ -110,17 +112,47 @@ __device__ __forceinline__ uint32_t byte_of(unsigned long long w, int i) {
     return (uint32_t)(w >> (8 * i)) & 0xffu;
 }
 
-__global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
-    const int y = blockIdx.x, frame = blockIdx.y, lane = threadIdx.x;
+// the step's zeroed int arrays, grid-strided over the launch's threads
+__device__ __forceinline__ void zero_arrays(const RowScanArgs &a, long long i0, long long nt) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        for (long long i = i0; i < a.zero_n[k]; i += nt) a.zero[k][i] = 0;
+}
+
+// a row's dword at x0 (4-B aligned: frame and stride are); the row's last
+// partial dword byte by byte, so no load reads past column W - 1 (a device
+// caller's buffer may end at the last row's W-th byte).  The bytes past W
+// read as 0 and are never used (x = W - 1 clamps x + 1 to itself).
+__device__ __forceinline__ uint32_t ld4(const uint8_t *row, int x0, int W) {
+    if (x0 + 4 <= W) return *reinterpret_cast<const uint32_t *>(row + x0);
+    uint32_t v = 0u;
+    for (int k = 0; k < 4 && x0 + k < W; k++) v |= (uint32_t)row[x0 + k] << (8 * k);
+    return v;
+}
+
+// bytes x0-1 .. x0+4 of a row around this lane's dword v (lanes l-1 / l+1 by
+// wave_shr / wave_shl; lane 0's left byte and lane 63's right byte come in)
+__device__ __forceinline__ unsigned long long byte_window(uint32_t v, uint32_t left, uint32_t right) {
+    const uint32_t l = (uint32_t)__builtin_amdgcn_update_dpp((int)(left << 24), (int)v, 0x138, 0xf, 0xf, false) >> 24;
+    const uint32_t r = (uint32_t)__builtin_amdgcn_update_dpp((int)right, (int)v, 0x130, 0xf, 0xf, false) & 0xffu;
+    return ((unsigned long long)r << 40) | ((unsigned long long)v << 8) | l;
+}
+
+// The 8 T2bFilter gradients of column x0 + j (j = 0..3) from the byte
+// windows of rows y-1, y, y+1, accumulated into G (x = W-1: x+1 clamps to x)
+__device__ __forceinline__ void grad8(unsigned long long U, unsigned long long C, unsigned long long D, int j,
+                                      bool last, uint32_t (&G)[8]) {
+    const int il = j, im = j + 1, ir = last ? j + 1 : j + 2;
+    // half 0: (C[x-1], C[x+1]), (U[x], D[x]); half 1: (U[x-1], D[x+1]), (D[x-1], U[x+1])
+    const uint32_t a0 = byte_of(C, il), b0 = byte_of(C, ir), c0_ = byte_of(U, im), d0_ = byte_of(D, im);
+    const uint32_t a1 = byte_of(U, il), b1 = byte_of(D, ir), c1_ = byte_of(D, il), d1_ = byte_of(U, ir);
+    G[0] += sat_sub(a0, b0); G[1] += sat_sub(b0, a0); G[2] += sat_sub(c0_, d0_); G[3] += sat_sub(d0_, c0_);
+    G[4] += sat_sub(a1, b1); G[5] += sat_sub(b1, a1); G[6] += sat_sub(c1_, d1_); G[7] += sat_sub(d1_, c1_);
+}
+
+__device__ __forceinline__ void rowcarry4_row(const RowScanArgs &a, int y, int frame, int lane) {
     const TableGeom g = a.g;
     const int W = g.W, H = g.H, ns = (W + kStrip - 1) / kStrip;
-    {   // the step's zeroed int arrays, grid-strided over the workgroups
-        const long long nt = (long long)gridDim.x * gridDim.y * 64;
-        const long long i0 = ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 64 + lane;
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            for (long long i = i0; i < a.zero_n[k]; i += nt) a.zero[k][i] = 0;
-    }
     const uint8_t *img = a.frames + (long long)frame * a.frame_bytes;
     float4 *tab = a.table + (long long)frame * g.frame4;
     const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -133,24 +165,14 @@ __global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
     const uint8_t *rd = img + (long long)(y < H - 1 ? y + 1 : H - 1) * a.stride;
     uint4 *out = reinterpret_cast<uint4 *>(a.carry) + ((long long)frame * H + y) * ns * 2;
     const int np = (W + 255) / 256;
-    // a row's dword at x0 (4-B aligned: frame and stride are); the row's last
-    // partial dword byte by byte, so no load reads past column W - 1 (a
-    // device caller's buffer may end at the last row's W-th byte).  The bytes
-    // past W read as 0 and are never used (x = W - 1 clamps x + 1 to itself).
-    auto ld4 = [&](const uint8_t *row, int x0) -> uint32_t {
-        if (x0 + 4 <= W) return *reinterpret_cast<const uint32_t *>(row + x0);
-        uint32_t v = 0u;
-        for (int k = 0; k < 4 && x0 + k < W; k++) v |= (uint32_t)row[x0 + k] << (8 * k);
-        return v;
-    };
     // a pass's dwords (rows u, c, d), loaded one pass ahead
     auto load = [&](int p, uint32_t &u, uint32_t &c, uint32_t &d) {
         const int x0 = p * 256 + 4 * lane;
         u = c = d = 0u;
         if (p < np && x0 < W) {
-            u = ld4(ru, x0);
-            c = ld4(rc, x0);
-            d = ld4(rd, x0);
+            u = ld4(ru, x0, W);
+            c = ld4(rc, x0, W);
+            d = ld4(rd, x0, W);
         }
     };
     uint32_t u0, c0, d0;
@@ -169,27 +191,14 @@ __global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
         const uint32_t nu = (uint32_t)__builtin_amdgcn_readlane((int)u1, 0) & 0xffu;
         const uint32_t nc = (uint32_t)__builtin_amdgcn_readlane((int)c1, 0) & 0xffu;
         const uint32_t nd = (uint32_t)__builtin_amdgcn_readlane((int)d1, 0) & 0xffu;
-        // bytes x0-1 .. x0+4 of each row (lanes l-1 / l+1 by wave_shr / wave_shl)
-        auto window = [&](uint32_t v, uint32_t left, uint32_t right) -> unsigned long long {
-            const uint32_t l = (uint32_t)__builtin_amdgcn_update_dpp((int)(left << 24), (int)v, 0x138, 0xf, 0xf, false) >> 24;
-            const uint32_t r = (uint32_t)__builtin_amdgcn_update_dpp((int)right, (int)v, 0x130, 0xf, 0xf, false) & 0xffu;
-            return ((unsigned long long)r << 40) | ((unsigned long long)v << 8) | l;
-        };
-        const unsigned long long U = window(u0, lu, nu), C = window(c0, lc, nc), D = window(d0, ld, nd);
+        const unsigned long long U = byte_window(u0, lu, nu), C = byte_window(c0, lc, nc), D = byte_window(d0, ld, nd);
         const int x0 = p * 256 + 4 * lane;
         uint32_t G[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
         uint32_t Pc[4][8];  // the lane's inclusive prefix through column j (R rows: rowfull's cells)
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int x = x0 + j;
-            if (x < W) {
-                const int il = j, im = j + 1, ir = x + 1 < W ? j + 2 : j + 1;  // x = W-1: x+1 clamps to x
-                // half 0: (C[x-1], C[x+1]), (U[x], D[x]); half 1: (U[x-1], D[x+1]), (D[x-1], U[x+1])
-                const uint32_t a0 = byte_of(C, il), b0 = byte_of(C, ir), c0_ = byte_of(U, im), d0_ = byte_of(D, im);
-                const uint32_t a1 = byte_of(U, il), b1 = byte_of(D, ir), c1_ = byte_of(D, il), d1_ = byte_of(U, ir);
-                G[0] += sat_sub(a0, b0); G[1] += sat_sub(b0, a0); G[2] += sat_sub(c0_, d0_); G[3] += sat_sub(d0_, c0_);
-                G[4] += sat_sub(a1, b1); G[5] += sat_sub(b1, a1); G[6] += sat_sub(c1_, d1_); G[7] += sat_sub(d1_, c1_);
-            }
+            if (x < W) grad8(U, C, D, j, x + 1 >= W, G);
 #pragma unroll
             for (int ch = 0; ch < 8; ch++) Pc[j][ch] = G[ch];
         }
@@ -235,6 +244,124 @@ __global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
         ld = (uint32_t)__builtin_amdgcn_readlane((int)d0, 63) >> 24;
         u0 = u1; c0 = c1; d0 = d1;
     }
+}
+
+__global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
+    zero_arrays(a, ((long long)blockIdx.y * gridDim.x + blockIdx.x) * 64 + threadIdx.x,
+                (long long)gridDim.x * gridDim.y * 64);
+    rowcarry4_row(a, blockIdx.x, blockIdx.y, threadIdx.x);
+}
+
+// One frame: rowcarry4's rows and the exact 32-row column-block sums of the
+// R rows (colseg's segment starts) in ONE launch.  A block sum is computed
+// from the pixels, not from the R rows rowcarry writes, so the two roles are
+// independent: sum_{y in blk} R_y(x+1) = sum_{x' <= x} (sum_{y in blk}
+// g_y(x')), i.e. the block's column sums of the 8 gradient planes, prefixed
+// along x once per block instead of once per row (exact u32: at most 32 *
+// 255 * W).  Workgroups [0, n_row_wg) are rowcarry4's (kRcbWaves rows each),
+// the others one block each: wave w takes the 256-column passes w, w +
+// kRcbWaves, ...; a pass's totals cross the waves through LDS for the
+// carry of the passes to its right.  Replaces colblock_kernel's launch and
+// its read of the R rows (50 MB at 1080p) by a read of the block's pixels.
+#ifndef SC_RCB_WAVES  // merged rowcarry4 + block-sum launch: waves per workgroup
+#define SC_RCB_WAVES 8
+#endif
+constexpr int kRcbWaves = SC_RCB_WAVES;
+constexpr int kCbRows = 8;  // block role: image rows whose loads are in flight together
+__device__ __forceinline__ void colblk_pixels(const RowScanArgs &a, int bb, int wv, int lane) {
+    const TableGeom g = a.g;
+    const int W = g.W, H = g.H, np = (W + 255) / 256;
+    const int y0 = bb * kColBlk, y1 = min(H, y0 + kColBlk);
+    const long long rs = (long long)g.rowp * 4;  // floats per table row (colblk's row stride)
+    __shared__ uint32_t s_tot[kRcbWaves][8];      // this chunk's pass totals
+    __shared__ uint32_t s_run[8];                 // the totals of the chunks done
+    if (threadIdx.x < 8) s_run[threadIdx.x] = 0u;
+    for (int c0 = 0; c0 < np; c0 += kRcbWaves) {
+        const int p = c0 + wv, x0 = p * 256 + 4 * lane;
+        uint32_t S[4][8];  // the block's column sums of the lane's 4 columns
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+            for (int ch = 0; ch < 8; ch++) S[j][ch] = 0u;
+        if (p < np) {
+            // lane 0's left byte: the previous pass's last (x = 0: itself);
+            // lane 63's right byte: the next pass's first
+            const int xl = p > 0 ? p * 256 - 1 : 0, xr = (p + 1) * 256;
+            for (int yb = y0; yb < y1; yb += kCbRows) {
+                // rows yb-1 .. yb+kCbRows (clamped like rowcarry's): loads first,
+                // in flight together, then the rows' gradients
+                uint32_t dw[kCbRows + 2], lb[kCbRows + 2], rb[kCbRows + 2];
+#pragma unroll
+                for (int k = 0; k < kCbRows + 2; k++) {
+                    const int yy = min(max(yb - 1 + k, 0), H - 1);
+                    const uint8_t *row = a.frames + (long long)yy * a.stride;
+                    dw[k] = x0 < W ? ld4(row, x0, W) : 0u;
+                    lb[k] = row[xl];
+                    rb[k] = xr < W ? row[xr] : 0u;
+                }
+#pragma unroll
+                for (int k = 0; k < kCbRows; k++) {
+                    if (yb + k >= y1) break;
+                    const unsigned long long Uw = byte_window(dw[k], lb[k], rb[k]);
+                    const unsigned long long Cw = byte_window(dw[k + 1], lb[k + 1], rb[k + 1]);
+                    const unsigned long long Dw = byte_window(dw[k + 2], lb[k + 2], rb[k + 2]);
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (x0 + j < W) grad8(Uw, Cw, Dw, j, x0 + j + 1 >= W, S[j]);
+                }
+            }
+        }
+        // in-pass inclusive prefix along x: the lane's 4 columns, then the wave
+        uint32_t E[8], T[8];
+#pragma unroll
+        for (int ch = 0; ch < 8; ch++) {
+            S[1][ch] += S[0][ch];
+            S[2][ch] += S[1][ch];
+            S[3][ch] += S[2][ch];
+            const uint32_t incl = wave_scan(S[3][ch]);
+            E[ch] = incl - S[3][ch];  // the pass's columns left of this lane
+            T[ch] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+        if (lane == 0)
+#pragma unroll
+            for (int ch = 0; ch < 8; ch++) s_tot[wv][ch] = p < np ? T[ch] : 0u;
+        __syncthreads();
+        if (p < np) {
+            uint32_t cy[8];  // every column left of this pass, over the block's rows
+#pragma unroll
+            for (int ch = 0; ch < 8; ch++) {
+                cy[ch] = s_run[ch] + E[ch];
+                for (int w2 = 0; w2 < wv; w2++) cy[ch] += s_tot[w2][ch];
+            }
+            uint4 *row = reinterpret_cast<uint4 *>(a.colblk + (long long)bb * rs);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int x = x0 + j;
+                if (x < W) {
+                    row[g.at(x + 1, 0)] = make_uint4(cy[0] + S[j][0], cy[1] + S[j][1], cy[2] + S[j][2], cy[3] + S[j][3]);
+                    row[g.at(x + 1, 1)] = make_uint4(cy[4] + S[j][4], cy[5] + S[j][5], cy[6] + S[j][6], cy[7] + S[j][7]);
+                }
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 8) {
+            uint32_t t = 0u;
+            for (int w2 = 0; w2 < kRcbWaves; w2++) t += s_tot[w2][threadIdx.x];
+            s_run[threadIdx.x] += t;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(64 * kRcbWaves) void rowcarry4_colblk_kernel(RowScanArgs a, int n_row_wg) {
+    const int wv = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+    zero_arrays(a, (long long)blockIdx.x * 64 * kRcbWaves + threadIdx.x, (long long)gridDim.x * 64 * kRcbWaves);
+    if ((int)blockIdx.x < n_row_wg) {  // (the whole workgroup takes one role: the barriers below are the block role's)
+        const int y = (int)blockIdx.x * kRcbWaves + wv;
+        if (y < a.g.H) rowcarry4_row(a, y, 0, lane);
+        return;
+    }
+    colblk_pixels(a, (int)blockIdx.x - n_row_wg, wv, lane);
 }
 
 #ifndef SC_COL_XCD
@@ -471,7 +598,6 @@ __global__ __launch_bounds__(64) void colsum_plane_kernel(RowScanArgs a) {
 #ifndef SC_COLSEG  // row segments (colsum4's one walk: 0.053 ms per 1080p frame; 4: 0.048, 8: 0.049, profiles/r4/colseg)
 #define SC_COLSEG 4
 #endif
-constexpr int kColBlk = 32;
 __global__ __launch_bounds__(64) void colblock_kernel(RowScanArgs a) {
     const TableGeom g = a.g;
     const int fi = blockIdx.x * 64 + threadIdx.x, blk = blockIdx.y;  // float within a table row
@@ -535,9 +661,29 @@ int colseg_segments() { return SC_COLSEG; }
 #ifndef SC_RC_DWORD  // rowcarry4 (dword loads) when the rows start 4-B aligned
 #define SC_RC_DWORD 1
 #endif
-bool launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
+// colseg's row segments for a frame of height H: seg rows each (a multiple of
+// kColBlk), nseg of them; block sums are needed above the last one's start
+__host__ __device__ inline void colseg_geometry(int H, int &seg, int &nseg) {
+    seg = ((H + SC_COLSEG - 1) / SC_COLSEG + kColBlk - 1) / kColBlk * kColBlk;
+    nseg = (H + seg - 1) / seg;
+}
+
+#ifndef SC_RC_COLBLK  // one frame: the column-block sums inside rowcarry4's launch (from the pixels)
+#define SC_RC_COLBLK 1
+#endif
+bool launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s, bool *colblk_done) {
     const bool aligned = ((uintptr_t)a.frames & 3u) == 0 && (a.stride & 3) == 0;
+    if (colblk_done) *colblk_done = false;
     if (SC_RC_DWORD && aligned) {
+        int seg = 0, nseg = 0;
+        colseg_geometry(a.g.H, seg, nseg);
+        if (SC_RC_COLBLK && SC_COLSEG > 1 && n_frames == 1 && a.colblk && nseg > 1) {
+            const int n_row_wg = (a.g.H + kRcbWaves - 1) / kRcbWaves, nblk = (nseg - 1) * seg / kColBlk;
+            hipLaunchKernelGGL(rowcarry4_colblk_kernel, dim3(n_row_wg + nblk), dim3(64 * kRcbWaves), 0, s, a,
+                               n_row_wg);
+            if (colblk_done) *colblk_done = true;
+            return a.rfull_n > 0;
+        }
         hipLaunchKernelGGL(rowcarry4_kernel, dim3(a.g.H, n_frames), dim3(64), 0, s, a);
         return a.rfull_n > 0;
     }
@@ -547,7 +693,7 @@ bool launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s) {
     return false;
 }
 
-void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s, bool have_r) {
+void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s, bool have_r, bool colblk_done) {
     const int ns64 = (a.g.W + 2 * kStrip - 1) / (2 * kStrip);
     if (two_pass) {
         if (!have_r)  // (rowcarry4 wrote the R rows already)
@@ -558,10 +704,11 @@ void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream
         if (SC_COLSUM_PLANE && n_frames >= 2) {
             hipLaunchKernelGGL(colsum_plane_kernel, dim3(a.g.rowp / 16, n_frames), dim3(64), 0, s, a);
         } else if (SC_COLSEG > 1 && n_frames == 1 && a.colblk) {
-            const int seg = ((a.g.H + SC_COLSEG - 1) / SC_COLSEG + kColBlk - 1) / kColBlk * kColBlk;
-            const int nseg = (a.g.H + seg - 1) / seg;
-            // (block sums only above the last segment's start: nothing reads the rest)
-            if (nseg > 1)
+            int seg = 0, nseg = 0;
+            colseg_geometry(a.g.H, seg, nseg);
+            // (block sums only above the last segment's start: nothing reads the
+            // rest; computed by rowcarry4's launch unless the frame took rowcarry)
+            if (nseg > 1 && !colblk_done)
                 hipLaunchKernelGGL(colblock_kernel, dim3(a.g.rowp / 16, (nseg - 1) * seg / kColBlk), dim3(64), 0, s, a);
             hipLaunchKernelGGL(colseg_kernel, dim3(a.g.rowp / 16, nseg), dim3(64), 0, s, a, seg);
         } else if (SC_COLSUM4) {

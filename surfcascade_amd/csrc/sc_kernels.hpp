@@ -259,9 +259,11 @@ void launch_features(const FeatureArgs &a, hipStream_t s);
 
 // integral pass 1 (rowcarry4 / rowcarry), sc_integral.hip; returns whether
 // the R rows of frames [0, a.rfull_n) were written (rowcarry4)
-bool launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s);
+// *colblk_done: the one-frame column-block sums (a.colblk) were computed in the same launch
+bool launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s, bool *colblk_done = nullptr);
 // two_pass: rowfull + colsum (small batches; rowfull skipped when have_r), else colstrip
-void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s, bool have_r = false);
+void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s, bool have_r = false,
+                    bool colblk_done = false);
 int colseg_segments();  // row segments of the one-frame column pass (0: colsum4)
 // Per-detector launch configuration: the device's CU count (queried once
 // per detector, no process-wide cache) and the SC_OPT_* launch options.

@@ -1407,16 +1407,26 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hi
     // at 16 waves).  C2 as a whole: -2.7 % (profiles/r3/g3).
     // One-frame launches (the latency path): 12 (0.656 vs 0.673 ms per 1080p
     // frame, profiles/r3/g12), the hand-off fill and drain dominate them.
+    // Tables beyond the Infinity Cache (a 4K frame's 265 MB) with 2+ frames
+    // per launch: 8 (fewer rows in flight per XCD: C4 24.92 vs 25.26 ms per
+    // launch at 12; its widest levels 24-31 alone 7.58 vs 7.85 ms, levels 0-23
+    // 19.30 vs 18.45, profiles/r5/e).
     const bool fabric_bound = a.g.frame4 * 16 > (128ll << 20);
-    int nw = !fabric_bound && a.n_frames > 1 && model_lds_bytes(a.K, true) + scratch(16) <= kLds ? 16 : 12;
-    if (c.chain_waves == 12 || (c.chain_waves == 16 && model_lds_bytes(a.K, false) + scratch(16) <= kLds))
-        nw = c.chain_waves;  // SC_OPT_CHAIN_WAVES
+    int nw = !fabric_bound && a.n_frames > 1 && model_lds_bytes(a.K, true) + scratch(16) <= kLds ? 16
+             : fabric_bound && a.n_frames > 1                                                  ? 8
+                                                                                               : 12;
+    if (c.chain_waves == 8 || c.chain_waves == 12 ||
+        (c.chain_waves == 16 && model_lds_bytes(a.K, false) + scratch(16) <= kLds))
+        nw = c.chain_waves;  // SC_OPT_CHAIN_WAVES (8: fewer rows in flight per XCD, A/B only)
     bool lw = model_lds_bytes(a.K, true) + scratch(nw) <= kLds;
     if (c.lds_weights >= 0) lw = lw && c.lds_weights != 0;  // SC_OPT_LDS_WEIGHTS
     const size_t lds = model_lds_bytes(a.K, lw) + scratch(nw);
     const int nt = 64 * nw;
     int per_cu = 0;
-    if (nw == 16 && lw)
+    if (nw == 8)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lw ? chain_kernel<true, 8> : chain_kernel<false, 8>,
+                                                           nt, lds);
+    else if (nw == 16 && lw)
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<true, 16>, nt, lds);
     else if (nw == 16)
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<false, 16>, nt, lds);
@@ -1428,7 +1438,11 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hi
     if (c.wgs_per_cu > 0) per_cu = std::min(per_cu, c.wgs_per_cu);  // SC_OPT_WGS_PER_CU
     const int grid = std::max(1, c.cus) * per_cu;
     if (waves_out) *waves_out = nw;
-    if (nw == 16 && lw)
+    if (nw == 8 && lw)
+        hipLaunchKernelGGL((chain_kernel<true, 8>), dim3(grid), dim3(nt), lds, s, a, w);
+    else if (nw == 8)
+        hipLaunchKernelGGL((chain_kernel<false, 8>), dim3(grid), dim3(nt), lds, s, a, w);
+    else if (nw == 16 && lw)
         hipLaunchKernelGGL((chain_kernel<true, 16>), dim3(grid), dim3(nt), lds, s, a, w);
     else if (nw == 16)
         hipLaunchKernelGGL((chain_kernel<false, 16>), dim3(grid), dim3(nt), lds, s, a, w);

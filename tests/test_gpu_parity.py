@@ -137,11 +137,12 @@ def test_phase_planes_and_workgroups(sc, oracle, face_cascade, phases, wgs, full
                  oracle.Params(n_levels=8), **opts)
 
 
-@pytest.mark.parametrize("waves,lw", [("12", None), ("16", None), ("16", "0"), ("12", "0")])
+@pytest.mark.parametrize("waves,lw", [("12", None), ("16", None), ("16", "0"), ("12", "0"), ("8", None), ("8", "0")])
 def test_chain_waves(sc, oracle, face_cascade, waves, lw):
-    """SC_OPT_CHAIN_WAVES: the 12-wave (3 per SIMD) and 16-wave (4 per SIMD,
-    rematerialised lane values, 128 VGPRs) chain kernels, with the weights in
-    LDS or read through the caches, give the oracle's bits."""
+    """SC_OPT_CHAIN_WAVES: the 8-wave (A/B only), 12-wave (3 per SIMD) and
+    16-wave (4 per SIMD, rematerialised lane values, 128 VGPRs) chain
+    kernels, with the weights in LDS or read through the caches, give the
+    oracle's bits."""
     opts = {"chain_waves": int(waves)}
     if lw:
         opts["lds_weights"] = int(lw)
@@ -196,7 +197,8 @@ def test_integral_batch_frames(sc, oracle, n):
 
 @pytest.mark.parametrize("n,opts", [(2, {"integral_fuse": 2, "integral_pre": 1}), (5, {"integral_pre": 2}),
                                     (7, {"chain_chunk": 3, "integral_fuse": 2}), (4, {}),
-                                    (4, {"integral_fuse": 1}), (6, {"integral_pre": 1, "chain_waves": 12})])
+                                    (4, {"integral_fuse": 1}), (6, {"integral_pre": 1, "chain_waves": 12}),
+                                    (5, {"chain_waves": 8})])
 def test_fused_integral(sc, oracle, face_cascade, n, opts):
     """The integral's column walks inside the chain kernel (SC_OPT_INTEGRAL_FUSE,
     the default from 4 frames per launch): every frame's table, evaluated
