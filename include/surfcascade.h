@@ -246,7 +246,8 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
 #define SC_OPT_CHAIN_WAVES 17 /* chain kernel waves per CU: 0 auto (16 when the  */
                               /* model and their scratch fit the LDS, a        */
                               /* frame's table is <= 128 MiB and the launch    */
-                              /* has 2+ frames), 8, 12, 16                     */
+                              /* has 2+ frames; 10 for tables > 128 MiB),      */
+                              /* 8, 10, 12, 14, 16                             */
 #define SC_OPT_INTEGRAL_FUSE 18 /* integral column walks inside the chain      */
                               /* kernel: 0 auto (from 4 frames per launch),   */
                               /* 1 never, 2 whenever a launch has 2+ frames    */

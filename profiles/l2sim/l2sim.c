@@ -118,6 +118,11 @@ static void item_cells(const Geom *g, const int32_t *rect, float scale, int y, i
  * levels); big_slots < 0: one queue. */
 static int g_cell_bytes = 16; /* 12: u24-packed half cells (lossless for values < 2^24) */
 void l2sim_set_cell_bytes(int b) { g_cell_bytes = b; }
+/* cu_chunk > 0: a CU takes cu_chunk consecutive queue tasks at a time into
+ * its own sub-queue (an LDS queue per workgroup), its slots then take tasks
+ * from it: the tasks in flight on one CU are neighbouring rows */
+static int g_cu_chunk = 0;
+void l2sim_set_cu_chunk(int c) { g_cu_chunk = c; }
 int l2sim_run(const Geom *g, int n_tasks, const int64_t *it_off, const int32_t *items,
               const int32_t *rects, const float *scale, int conc, int cus, int l1_lines,
               int l2_lines, const int32_t *xcd_of_task, const int32_t *grp_of_level, int n_groups,
@@ -147,9 +152,15 @@ int l2sim_run(const Geom *g, int n_tasks, const int64_t *it_off, const int32_t *
             else qs[ns++] = q[i];
         }
         int next = 0, live = 0;
+        const int chunk = g_cu_chunk > 0 ? g_cu_chunk : 1;
+        int *cq = malloc(sizeof(int) * cus * chunk), *cqn = calloc(cus, sizeof(int)), *cqi = calloc(cus, sizeof(int));
         /* next task for slot s (-1: none) */
+#define TAKE_CU(cu_) \
+        (cqi[cu_] < cqn[cu_] ? cq[(cu_) * chunk + cqi[cu_]++] \
+         : (cqn[cu_] = 0, cqi[cu_] = 0, ({ while (cqn[cu_] < chunk && next < nt) cq[(cu_) * chunk + cqn[cu_]++] = q[next++]; 0; }), \
+            cqi[cu_] < cqn[cu_] ? cq[(cu_) * chunk + cqi[cu_]++] : -1))
 #define TAKE(s_)                                                                        \
-        ((big_slots < 0) ? (next < nt ? q[next++] : -1)                                 \
+        ((big_slots < 0) ? (g_cu_chunk > 0 ? TAKE_CU((s_) % cus) : (next < nt ? q[next++] : -1)) \
          : ((s_) < big_slots                                                             \
                 ? ((is < ns && (ib >= nb || qs[is] < qb[ib])) ? qs[is++] : (ib < nb ? qb[ib++] : -1)) \
                 : (is < ns ? qs[is++] : -1)))
@@ -210,6 +221,9 @@ int l2sim_run(const Geom *g, int n_tasks, const int64_t *it_off, const int32_t *
                 }
             }
         }
+        free(cq);
+        free(cqn);
+        free(cqi);
         free(qs);
         free(qb);
         free(act);

@@ -1640,8 +1640,9 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
             case SC_OPT_CHAIN_SUBQ: o.chain_subq = range(0, sc::kMaxSubQ); regeo = false; break;
             case SC_OPT_CHAIN_WAVES:
                 o.chain_waves = range(0, 16);
-                if (o.chain_waves != 0 && o.chain_waves != 8 && o.chain_waves != 12 && o.chain_waves != 16)
-                    throw Error{SC_ERR_INVALID, "chain_waves: 0, 8, 12 or 16"};
+                if (o.chain_waves != 0 && o.chain_waves != 8 && o.chain_waves != 10 && o.chain_waves != 12 &&
+                    o.chain_waves != 14 && o.chain_waves != 16)
+                    throw Error{SC_ERR_INVALID, "chain_waves: 0, 8, 10, 12, 14 or 16"};
                 regeo = false;
                 break;
             case SC_OPT_LEVEL_LO: o.level_lo = range(0, 256); break;

@@ -264,10 +264,13 @@ __global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
 // carry of the passes to its right.  Replaces colblock_kernel's launch and
 // its read of the R rows (50 MB at 1080p) by a read of the block's pixels.
 #ifndef SC_RCB_WAVES  // merged rowcarry4 + block-sum launch: waves per workgroup
-#define SC_RCB_WAVES 8
+#define SC_RCB_WAVES 8  // (one frame: rowscan + colseg 0.0608 ms; 4: 0.0724, 16: 0.0665; profiles/r5/f)
 #endif
 constexpr int kRcbWaves = SC_RCB_WAVES;
-constexpr int kCbRows = 8;  // block role: image rows whose loads are in flight together
+#ifndef SC_CB_ROWS  // block role: image rows whose loads are in flight together
+#define SC_CB_ROWS 8
+#endif
+constexpr int kCbRows = SC_CB_ROWS;
 __device__ __forceinline__ void colblk_pixels(const RowScanArgs &a, int bb, int wv, int lane) {
     const TableGeom g = a.g;
     const int W = g.W, H = g.H, np = (W + 255) / 256;

@@ -1408,16 +1408,17 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hi
     // One-frame launches (the latency path): 12 (0.656 vs 0.673 ms per 1080p
     // frame, profiles/r3/g12), the hand-off fill and drain dominate them.
     // Tables beyond the Infinity Cache (a 4K frame's 265 MB) with 2+ frames
-    // per launch: 8 (fewer rows in flight per XCD: C4 24.92 vs 25.26 ms per
-    // launch at 12; its widest levels 24-31 alone 7.58 vs 7.85 ms, levels 0-23
-    // 19.30 vs 18.45, profiles/r5/e).
+    // per launch: 10 (fewer rows in flight per XCD: C4 24.70 ms per launch vs
+    // 24.92 at 8 and 25.22 at 12, profiles/r5/f; at 8 its widest levels 24-31
+    // alone 7.58 vs 7.85 ms, levels 0-23 19.30 vs 18.45, profiles/r5/e).
     const bool fabric_bound = a.g.frame4 * 16 > (128ll << 20);
     int nw = !fabric_bound && a.n_frames > 1 && model_lds_bytes(a.K, true) + scratch(16) <= kLds ? 16
-             : fabric_bound && a.n_frames > 1                                                  ? 8
+             : fabric_bound && a.n_frames > 1                                                  ? 10
                                                                                                : 12;
-    if (c.chain_waves == 8 || c.chain_waves == 12 ||
-        (c.chain_waves == 16 && model_lds_bytes(a.K, false) + scratch(16) <= kLds))
-        nw = c.chain_waves;  // SC_OPT_CHAIN_WAVES (8: fewer rows in flight per XCD, A/B only)
+    if (c.chain_waves == 8 || c.chain_waves == 10 || c.chain_waves == 12 ||
+        ((c.chain_waves == 14 || c.chain_waves == 16) &&
+         model_lds_bytes(a.K, false) + scratch(c.chain_waves) <= kLds))
+        nw = c.chain_waves;  // SC_OPT_CHAIN_WAVES (10 / 14: A/B only)
     bool lw = model_lds_bytes(a.K, true) + scratch(nw) <= kLds;
     if (c.lds_weights >= 0) lw = lw && c.lds_weights != 0;  // SC_OPT_LDS_WEIGHTS
     const size_t lds = model_lds_bytes(a.K, lw) + scratch(nw);
@@ -1425,6 +1426,12 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hi
     int per_cu = 0;
     if (nw == 8)
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lw ? chain_kernel<true, 8> : chain_kernel<false, 8>,
+                                                           nt, lds);
+    else if (nw == 10)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lw ? chain_kernel<true, 10> : chain_kernel<false, 10>,
+                                                           nt, lds);
+    else if (nw == 14)
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lw ? chain_kernel<true, 14> : chain_kernel<false, 14>,
                                                            nt, lds);
     else if (nw == 16 && lw)
         (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, chain_kernel<true, 16>, nt, lds);
@@ -1438,7 +1445,15 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hi
     if (c.wgs_per_cu > 0) per_cu = std::min(per_cu, c.wgs_per_cu);  // SC_OPT_WGS_PER_CU
     const int grid = std::max(1, c.cus) * per_cu;
     if (waves_out) *waves_out = nw;
-    if (nw == 8 && lw)
+    if (nw == 10 && lw)
+        hipLaunchKernelGGL((chain_kernel<true, 10>), dim3(grid), dim3(nt), lds, s, a, w);
+    else if (nw == 10)
+        hipLaunchKernelGGL((chain_kernel<false, 10>), dim3(grid), dim3(nt), lds, s, a, w);
+    else if (nw == 14 && lw)
+        hipLaunchKernelGGL((chain_kernel<true, 14>), dim3(grid), dim3(nt), lds, s, a, w);
+    else if (nw == 14)
+        hipLaunchKernelGGL((chain_kernel<false, 14>), dim3(grid), dim3(nt), lds, s, a, w);
+    else if (nw == 8 && lw)
         hipLaunchKernelGGL((chain_kernel<true, 8>), dim3(grid), dim3(nt), lds, s, a, w);
     else if (nw == 8)
         hipLaunchKernelGGL((chain_kernel<false, 8>), dim3(grid), dim3(nt), lds, s, a, w);

@@ -137,9 +137,10 @@ def test_phase_planes_and_workgroups(sc, oracle, face_cascade, phases, wgs, full
                  oracle.Params(n_levels=8), **opts)
 
 
-@pytest.mark.parametrize("waves,lw", [("12", None), ("16", None), ("16", "0"), ("12", "0"), ("8", None), ("8", "0")])
+@pytest.mark.parametrize("waves,lw", [("12", None), ("16", None), ("16", "0"), ("12", "0"), ("8", None), ("8", "0"),
+                                     ("10", None), ("14", None)])
 def test_chain_waves(sc, oracle, face_cascade, waves, lw):
-    """SC_OPT_CHAIN_WAVES: the 8-wave (A/B only), 12-wave (3 per SIMD) and
+    """SC_OPT_CHAIN_WAVES: the 8-, 10- and 14-wave (A/B), 12-wave (3 per SIMD) and
     16-wave (4 per SIMD, rematerialised lane values, 128 VGPRs) chain
     kernels, with the weights in LDS or read through the caches, give the
     oracle's bits."""
