@@ -418,6 +418,7 @@ class Detector:
     """Owns device model + buffers + one HIP stream (sc_detector)."""
 
     _stream = None  # the stream object set_stream launches on (kept alive while in use)
+    _sp_cache = None  # the detector's stream handle (refreshed by set_stream)
 
     def __init__(self, cascade, params: ScanParams | None = None, device: int = 0):
         L = load_library()
@@ -487,24 +488,33 @@ class Detector:
             raise ValueError("frames must be row-major [n, H, W] (strides %s)" % (frames.stride(),))
         return n, H, W, s1
 
+    def _cur_stream(self):
+        """torch's current stream on this device (raw handle; the Stream
+        object torch.cuda.current_stream builds costs microseconds per call,
+        which a one-frame call pays before its first kernel launches)."""
+        import torch
+        raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        return raw(self.device) if raw is not None else torch.cuda.current_stream(self.device).cuda_stream
+
     def _after_torch(self, *tensors):
         """Order the detector's stream after the work torch has queued on the
         current stream of this device (producers of `tensors`, earlier frees):
         sc_detector_wait_stream, no host sync.  Every tensor must live on the
-        detector's GPU."""
-        import torch
+        detector's GPU.  Returns torch's current stream (raw handle)."""
         for t in tensors:
-            if t is not None and (not t.is_cuda or t.device.index != self.device):
+            if t is not None and t.get_device() != self.device:
                 raise ValueError("tensor on %s, detector on cuda:%d" % (t.device, self.device))
-        s = torch.cuda.current_stream(self.device).cuda_stream
-        if s != (self.stream_ptr or 0):  # (a detector on torch's current stream is ordered already)
+        s = self._cur_stream()
+        if s != self._sp:  # (a detector on torch's current stream is ordered already)
             _check(load_library().sc_detector_wait_stream(self._h, s))
+        return s
 
-    def _before_torch(self):
-        """Order torch's current stream after the detector's queued work."""
-        import torch
-        s = torch.cuda.current_stream(self.device).cuda_stream
-        if s != (self.stream_ptr or 0):
+    def _before_torch(self, s=None):
+        """Order torch's current stream (raw handle s, or looked up) after the
+        detector's queued work."""
+        if s is None:
+            s = self._cur_stream()
+        if s != self._sp:
             _check(load_library().sc_stream_wait_detector(self._h, s))
 
     def detect_device(self, frames, capacity=1 << 18):
@@ -527,11 +537,11 @@ class Detector:
         n, H, W, rs = self._device_frames(frames)
         if counts.dtype != __import__("torch").int32 or counts.numel() < 1 + n:
             raise ValueError("counts must be an int32 tensor of at least 1 + n values")
-        self._after_torch(frames, out_records, counts)
+        s = self._after_torch(frames, out_records, counts)
         cap = out_records.numel() * out_records.element_size() // RECORD_DTYPE.itemsize
         _check(load_library().sc_enqueue_device(self._h, frames.data_ptr(), n, W, H, rs,
                                                 out_records.data_ptr(), cap, counts.data_ptr()))
-        self._before_torch()
+        self._before_torch(s)
 
     def synchronize(self):
         _check(load_library().sc_synchronize(self._h))
@@ -539,6 +549,12 @@ class Detector:
     @property
     def stream_ptr(self):
         return load_library().sc_detector_stream(self._h)
+
+    @property
+    def _sp(self):  # the detector's stream as a raw int (0: the null stream), cached
+        if self._sp_cache is None:
+            self._sp_cache = self.stream_ptr or 0
+        return self._sp_cache
 
     def set_stream(self, stream=None):
         """Launch on `stream` (a torch.cuda.Stream, or a raw hipStream_t of the
@@ -548,6 +564,7 @@ class Detector:
         the stream object until set_stream(None) or close(), because it
         synchronises that stream when destroyed; a raw handle must stay valid
         for as long itself (the caller owns it)."""
+        self._sp_cache = None
         if stream is None:
             _check(load_library().sc_detector_set_stream(self._h, None, 1))
             self._stream = None

@@ -271,6 +271,16 @@ constexpr int kRcbWaves = SC_RCB_WAVES;
 #define SC_CB_ROWS 8
 #endif
 constexpr int kCbRows = SC_CB_ROWS;
+#ifndef SC_CB_SBYTES
+#define SC_CB_SBYTES 0
+#endif
+// byte i of a row at a wave-uniform address, by a scalar dword load
+__device__ __forceinline__ uint32_t sbyte(const uint8_t *row, int i) {
+    typedef __attribute__((address_space(4))) const uint32_t cu32;
+    const unsigned long long p = (unsigned long long)(row + i);
+    const uint32_t w = *(cu32 *)(p & ~3ull);
+    return (w >> (8 * (unsigned)(p & 3ull))) & 0xffu;
+}
 __device__ __forceinline__ void colblk_pixels(const RowScanArgs &a, int bb, int wv, int lane) {
     const TableGeom g = a.g;
     const int W = g.W, H = g.H, np = (W + 255) / 256;
@@ -299,8 +309,13 @@ __device__ __forceinline__ void colblk_pixels(const RowScanArgs &a, int bb, int 
                     const int yy = min(max(yb - 1 + k, 0), H - 1);
                     const uint8_t *row = a.frames + (long long)yy * a.stride;
                     dw[k] = x0 < W ? ld4(row, x0, W) : 0u;
+#if SC_CB_SBYTES  // the wave-uniform neighbour bytes through the scalar cache (the frame is read-only here)
+                    lb[k] = sbyte(row, xl);
+                    rb[k] = xr < W ? sbyte(row, xr) : 0u;
+#else
                     lb[k] = row[xl];
                     rb[k] = xr < W ? row[xr] : 0u;
+#endif
                 }
 #pragma unroll
                 for (int k = 0; k < kCbRows; k++) {
@@ -598,8 +613,13 @@ __global__ __launch_bounds__(64) void colsum_plane_kernel(RowScanArgs a) {
 // wave only: the pass is in place).  The same bits as the sequential walk for
 // every input; the walk is as long as the column's last exact segment start
 // allows (a 1080p bench frame passes 2^24 from row 939 on).
-#ifndef SC_COLSEG  // row segments (colsum4's one walk: 0.053 ms per 1080p frame; 4: 0.048, 8: 0.049, profiles/r4/colseg)
-#define SC_COLSEG 4
+// row segments: 5 (column pass 0.0314 ms per 1080p frame with the block sums
+// from rowcarry4's launch; 4: 0.0334, 3: 0.0385, profiles/r5/h; colsum4's one
+// walk: 0.053).  More segments start later rows, and a column whose sum has
+// passed 2^24 above a start is walked on by its last exact segment: at 6 the
+// bench frames' last start (row 960) is past their 2^24 crossing (row 939)
+#ifndef SC_COLSEG
+#define SC_COLSEG 5
 #endif
 __global__ __launch_bounds__(64) void colblock_kernel(RowScanArgs a) {
     const TableGeom g = a.g;
