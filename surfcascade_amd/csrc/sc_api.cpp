@@ -158,7 +158,7 @@ struct sc_detector {
     PinnedBuf h_stage;           // host frames -> pinned -> d_frames (upload_frames)
     DevBuf<float4> d_table;
     DevBuf<uint32_t> d_carry;    // integral pass 1 -> pass 2: per-strip row prefixes
-    DevBuf<uint32_t> d_colblk;   // one-frame column pass: exact 32-row column sums (colseg)
+    DevBuf<uint32_t> d_colblk;   // one-frame column pass: exact column-block sums (colseg)
     int table_frames = 0;
     DevBuf<sc_det_record> d_out;
     DevBuf<int> d_counters;
@@ -724,7 +724,7 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     const bool two_pass_pre = d->opt.integral_passes ? d->opt.integral_passes == 2 : pre <= 3;
     ra.rfull_n = fuse ? (two_pass_pre ? std::min(pre, n) : 0) : (two_pass_all ? n : 0);
     if (n == 1 && two_pass_all && sc::colseg_segments() > 1) {
-        d->d_colblk.ensure((size_t)(g.H + 31) / 32 * g.tg.rowp * 4);
+        d->d_colblk.ensure((size_t)(g.H + sc::colblk_rows() - 1) / sc::colblk_rows() * g.tg.rowp * 4);
         ra.colblk = d->d_colblk.p;
     }
     d->spec_word = -1;  // (set by a chain launch below: SC_INFO_SPEC_ROUNDS reads 0 otherwise)

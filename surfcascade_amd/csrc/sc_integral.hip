@@ -40,7 +40,10 @@ constexpr int kColUnroll = SC_COL_UNROLL;  // rows per colstrip block (two block
 #define SC_COL_WAVES 1
 #endif
 
-constexpr int kColBlk = 32;  // one-frame column pass: rows per exact column-block sum (colseg)
+#ifndef SC_COLBLK  // one-frame column pass: rows per exact column-block sum (colseg's starts)
+#define SC_COLBLK 32
+#endif
+constexpr int kColBlk = SC_COLBLK;
 
 #ifndef SC_RC_ROWS  // rowcarry: rows (waves) per workgroup
 #define SC_RC_ROWS 1
@@ -680,6 +683,7 @@ __global__ __launch_bounds__(64) void colseg_kernel(RowScanArgs a, int seg_len) 
 }  // namespace
 
 int colseg_segments() { return SC_COLSEG; }
+int colblk_rows() { return kColBlk; }
 
 #ifndef SC_RC_DWORD  // rowcarry4 (dword loads) when the rows start 4-B aligned
 #define SC_RC_DWORD 1

@@ -265,6 +265,7 @@ bool launch_rowscan(const RowScanArgs &a, int n_frames, hipStream_t s, bool *col
 void launch_colscan(const RowScanArgs &a, int n_frames, bool two_pass, hipStream_t s, bool have_r = false,
                     bool colblk_done = false);
 int colseg_segments();  // row segments of the one-frame column pass (0: colsum4)
+int colblk_rows();      // rows per exact column-block sum of the one-frame column pass
 // Per-detector launch configuration: the device's CU count (queried once
 // per detector, no process-wide cache) and the SC_OPT_* launch options.
 struct LaunchCfg {
