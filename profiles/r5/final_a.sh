@@ -1,9 +1,8 @@
 #!/bin/bash
-# Round 5 evidence at HEAD (code frozen: the build id the PMC table is stamped
-# with is this tree's): the GPU suite, smoke, the default bench line (C2 with
-# the CPU baseline and the one-frame latency leg), C1 / C4 / C5 lines, the
-# rocprofv3 kernel-trace summaries of the default command and of one frame
-# per step, and the PMC passes of C2 / C4 / C5.
+# Round 5 evidence at HEAD, part A (code frozen): the GPU suite, smoke, the
+# default bench line (C2 with the CPU baseline and the one-frame latency leg),
+# C1 / C4 / C5 lines, rocprofv3 kernel-trace summaries of the default command
+# and of one frame per step.  Part B (final_b.sh): the PMC passes.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; O=gpurun_out/r5final; mkdir -p $R/$O; cd $R
 bash profiles/run.sh r5final pytest smoke || exit 1
@@ -12,5 +11,4 @@ python3 -c "import json;d=json.load(open('$O/bench.json'));print('C2', d['value'
 bash profiles/run.sh r5final "bench bench_C4 --config C4" "bench bench_C5 --config C5" "rocprof trace" \
   "rocprof trace_b1 --batch 1 --steps 50" || exit 1
 timeout -k 10 300 python3 bench.py --config C1 > $O/bench_C1.json 2> $O/bench_C1.err || exit 1
-for c in C2 C4 C5; do bash profiles/collect_pmc_cfg.sh $O/pmc/$c --config $c || exit 1; echo "pmc $c done"; done
-echo final done
+echo final_a done

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Copy gpurun_out/r5final into profiles/r5/final (tracked) and re-key
+# Copy gpurun_out/r5final (final_a.sh + final_b.sh) into profiles/r5/final (tracked) and re-key
 # profiles/pmc_windows.json (C2 / C4 / C5) on its PMC passes: each entry
 # carries the build id of the library the passes profiled.
 set -e
