@@ -255,13 +255,13 @@ __global__ __launch_bounds__(64) void rowcarry4_kernel(RowScanArgs a) {
     rowcarry4_row(a, blockIdx.x, blockIdx.y, threadIdx.x);
 }
 
-// One frame: rowcarry4's rows and the exact 32-row column-block sums of the
-// R rows (colseg's segment starts) in ONE launch.  A block sum is computed
+// One frame: rowcarry4's rows and the exact kColBlk-row column-block sums of
+// the R rows (colseg's segment starts) in ONE launch.  A block sum is computed
 // from the pixels, not from the R rows rowcarry writes, so the two roles are
 // independent: sum_{y in blk} R_y(x+1) = sum_{x' <= x} (sum_{y in blk}
 // g_y(x')), i.e. the block's column sums of the 8 gradient planes, prefixed
-// along x once per block instead of once per row (exact u32: at most 32 *
-// 255 * W).  Workgroups [0, n_row_wg) are rowcarry4's (kRcbWaves rows each),
+// along x once per block instead of once per row (exact u32: at most kColBlk
+// * 255 * W).  Workgroups [0, n_row_wg) are rowcarry4's (kRcbWaves rows each),
 // the others one block each: wave w takes the 256-column passes w, w +
 // kRcbWaves, ...; a pass's totals cross the waves through LDS for the
 // carry of the passes to its right.  Replaces colblock_kernel's launch and
@@ -274,16 +274,6 @@ constexpr int kRcbWaves = SC_RCB_WAVES;
 #define SC_CB_ROWS 8
 #endif
 constexpr int kCbRows = SC_CB_ROWS;
-#ifndef SC_CB_SBYTES
-#define SC_CB_SBYTES 0
-#endif
-// byte i of a row at a wave-uniform address, by a scalar dword load
-__device__ __forceinline__ uint32_t sbyte(const uint8_t *row, int i) {
-    typedef __attribute__((address_space(4))) const uint32_t cu32;
-    const unsigned long long p = (unsigned long long)(row + i);
-    const uint32_t w = *(cu32 *)(p & ~3ull);
-    return (w >> (8 * (unsigned)(p & 3ull))) & 0xffu;
-}
 __device__ __forceinline__ void colblk_pixels(const RowScanArgs &a, int bb, int wv, int lane) {
     const TableGeom g = a.g;
     const int W = g.W, H = g.H, np = (W + 255) / 256;
@@ -312,13 +302,8 @@ __device__ __forceinline__ void colblk_pixels(const RowScanArgs &a, int bb, int 
                     const int yy = min(max(yb - 1 + k, 0), H - 1);
                     const uint8_t *row = a.frames + (long long)yy * a.stride;
                     dw[k] = x0 < W ? ld4(row, x0, W) : 0u;
-#if SC_CB_SBYTES  // the wave-uniform neighbour bytes through the scalar cache (the frame is read-only here)
-                    lb[k] = sbyte(row, xl);
-                    rb[k] = xr < W ? sbyte(row, xr) : 0u;
-#else
-                    lb[k] = row[xl];
+                    lb[k] = row[xl];  // (wave-uniform; as scalar loads: +22 % rowscan, profiles/r5/h)
                     rb[k] = xr < W ? row[xr] : 0u;
-#endif
                 }
 #pragma unroll
                 for (int k = 0; k < kCbRows; k++) {
