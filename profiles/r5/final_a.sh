@@ -11,4 +11,5 @@ python3 -c "import json;d=json.load(open('$O/bench.json'));print('C2', d['value'
 bash profiles/run.sh r5final "bench bench_C4 --config C4" "bench bench_C5 --config C5" "rocprof trace" \
   "rocprof trace_b1 --batch 1 --steps 50" || exit 1
 timeout -k 10 300 python3 bench.py --config C1 > $O/bench_C1.json 2> $O/bench_C1.err || exit 1
+timeout -k 10 240 python3 profiles/r5/latency_legs.py > $O/legs.json 2> $O/legs.err || exit 1
 echo final_a done

@@ -112,48 +112,6 @@ __device__ __forceinline__ int2 row_desc(const int2 *rows, int i) {
     return make_int2((int)(unsigned)v, (int)(unsigned)(v >> 32));
 }
 
-// Hand-off polls (a segment's entry word, a frame's walk count): wave-uniform
-// 4-B reads of words other CUs store with agent scope.  SC_SPOLL 1 (default)
-// reads them through the scalar path with glc (the scalar cache is missed,
-// the value comes from L2, where the sc1 stores land), so a waiting wave's
-// polls stay off the texture data path the gathers keep busy: one frame's
-// chain kernel 0.589 -> 0.584 ms, C2 / C4 unchanged, 3.6 % fewer vector
-// loads at C2 (profiles/r5/l); 0: a one-lane sc1 vector load.  Both polls
-// are relaxed: the entry is the data itself, and a ready frame is followed
-// by an agent-scope acquire (frame_ready).  (Loads only: nothing is ever
-// stored through the scalar path.)
-#ifndef SC_SPOLL
-#define SC_SPOLL 1
-#endif
-#if SC_SPOLL
-__device__ __forceinline__ const int *uniform_ptr(const int *p) {
-    const unsigned long long a = (unsigned long long)p;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-    return reinterpret_cast<const int *>(((unsigned long long)hi << 32) | lo);
-}
-#endif
-__device__ __forceinline__ int poll_word(const int *p) {
-#if SC_SPOLL
-    int v;
-    // (the wait inside the statement: the compiler's own lgkmcnt waits do not
-    // count an SMEM load it did not issue)
-    asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(uniform_ptr(p)) : "memory");
-    return v;
-#else
-    int v = 0;
-    if (lead_lane()) v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return __builtin_amdgcn_readfirstlane(v);
-#endif
-}
-#if SC_SPOLL
-// two scalar polls in flight together (p1 may repeat p0 when one is wanted)
-__device__ __forceinline__ void poll_words2(const int *p0, const int *p1, int &v0, int &v1) {
-    asm volatile("s_load_dword %0, %2, 0x0 glc\n\ts_load_dword %1, %3, 0x0 glc\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&s"(v0), "=&s"(v1) : "s"(uniform_ptr(p0)), "s"(uniform_ptr(p1)) : "memory");
-}
-#endif
-
 // Bit i of m -> bit base + 2i of the bit array w (i < 64: the positions
 // k = r + 2u of a batch chunk's windows): the 32-bit halves of m spread to
 // every second bit of a 64-bit word, each ORed in at its offset.
@@ -902,7 +860,10 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         if (fr < c) return true;
         const int c0 = c;
         while (c < a.n_frames) {
-            if (poll_word(&w.int_ctl[1 + c]) < w.walks_per_frame) break;
+            int v = 0;
+            if (lead_lane())
+                v = __hip_atomic_load(&w.int_ctl[1 + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__builtin_amdgcn_readfirstlane(v) < w.walks_per_frame) break;
             c++;
         }
         if (c > c0) {
@@ -1050,15 +1011,6 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     st[sl] = 1;
                     if (tq[sl] == 0 || SC_ABL_NOWAIT) start(sl, j0[sl]);  // (segment 0 enters at 0)
                 }
-#if SC_SPOLL
-            static_assert(kSlots == 2, "two polls per statement");
-            e[0] = e[1] = 0;
-            if (st[0] == 1 || st[1] == 1) {
-                const int *p0 = &w.entry[(long long)tt[0] * nsg + tq[0]];
-                const int *p1 = &w.entry[(long long)tt[1] * nsg + tq[1]];
-                poll_words2(st[0] == 1 ? p0 : p1, st[1] == 1 ? p1 : p0, e[0], e[1]);
-            }
-#else
 #pragma unroll
             for (int sl = 0; sl < kSlots; sl++) {
                 e[sl] = 0;
@@ -1066,7 +1018,6 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     e[sl] = __hip_atomic_load(&w.entry[(long long)tt[sl] * nsg + tq[sl]], __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
             }
-#endif
 #pragma unroll
             for (int sl = 0; sl < kSlots; sl++) {
                 const int es = __builtin_amdgcn_readfirstlane(e[sl]);
