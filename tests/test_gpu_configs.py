@@ -249,6 +249,53 @@ def test_watchdog_ends_a_lost_walk_count(sc):
     assert "RAISED True" in r.stdout and "CLEAN AFTER" in r.stdout, r.stdout
 
 
+def _bench_form_exact(sc, oracle, cascade, model, W, H, n, params_sc, params_or, expect, full_frames):
+    """One sc_enqueue_device call over bench.py's n device-resident frames
+    (seeds 1000..), the detector on torch's stream, the launch shape `expect`
+    (SC_INFO values) asserted; tables and per-window stage / score bits of
+    `full_frames`, the visited set and the detections of every frame."""
+    import torch
+    from surfcascade_amd import RECORD_DTYPE, synth
+    from surfcascade_amd.dist import merge_records
+    host = synth.make_frames(W, H, n, seed0=1000)  # bench.py's frames
+    frames = torch.from_numpy(host).to("cuda:0")
+    det = sc.Detector(model, params_sc)
+    det.set_stream(torch.cuda.current_stream())
+    det.set_debug(True)
+    recs = torch.zeros((1 << 18) * RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda:0")
+    counts = torch.zeros(n + 1, dtype=torch.int32, device="cuda:0")
+    det.enqueue_device(frames, recs, counts)
+    det.synchronize()
+    for k, v in expect.items():
+        assert det.info(k) == v, (k, det.info(k))
+    got = merge_records([counts.cpu().numpy()], [recs.cpu().numpy()], [0])
+    layout, _ = oracle.grid_layout(W, H, params_or)
+    vis_all, det_all = 0, 0
+    for f in range(n):
+        T = oracle.integral(host[f])
+        if f in full_frames:
+            assert det.dump_integral(W, H, frame=f).view(np.uint32).tobytes() == \
+                T.view(np.uint32).tobytes(), f
+        p, s, v = det.dump_grid(frame=f)
+        rp, rs = oracle.eval_grid(T, cascade, params_or)
+        if f in full_frames:
+            ev = p != -2
+            np.testing.assert_array_equal(p[ev], rp[ev])
+            assert s[ev].view(np.uint32).tobytes() == rs[ev].view(np.uint32).tobytes(), f
+        rv, _ = oracle.walk_grid(rp, rs, layout, cascade.n_stages, params_or.stride_score)
+        np.testing.assert_array_equal(v, rv)
+        ref, nv = oracle.detect(T, cascade, params_or)
+        assert nv == int(rv.sum())
+        mine = got[got["frame"] == f]
+        assert _det_set(mine) == _det_set(ref), f
+        vis_all += nv
+        det_all += len(ref)
+    assert det.info("visited") == vis_all
+    assert int(counts[0].item()) == det_all
+    det.set_stream(None)
+    return det_all
+
+
 def test_c2_bench_form_exact(sc, oracle, face_cascade):
     """C2 exactly as bench.py measures it: 32 device-resident 1080p frames x
     24 levels in ONE sc_enqueue_device call, the calibrated model
@@ -258,48 +305,32 @@ def test_c2_bench_form_exact(sc, oracle, face_cascade):
     per-window stage / score bits of frames 0 (prebuilt), 2 and 31 (fused),
     the visited set and the detections of every frame (VERDICT r4 next #2;
     ObjDetector.cpp:188-212)."""
-    import torch
-    from surfcascade_amd import RECORD_DTYPE, synth
-    from surfcascade_amd.dist import merge_records
-    host = synth.make_frames(1920, 1080, 32, seed0=1000)  # bench.py's frames (seeds 1000..1031)
-    frames = torch.from_numpy(host).to("cuda:0")
-    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=24))
-    det.set_stream(torch.cuda.current_stream())
-    det.set_debug(True)
-    recs = torch.zeros((1 << 18) * RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda:0")
-    counts = torch.zeros(33, dtype=torch.int32, device="cuda:0")
-    det.enqueue_device(frames, recs, counts)
-    det.synchronize()
-    assert det.info("fused_frames") == 30
-    assert det.info("chain_waves") == 16
-    assert det.info("chain_subq") == 1
-    assert det.info("column_pass") == 1
-    got = merge_records([counts.cpu().numpy()], [recs.cpu().numpy()], [0])
-    params = oracle.Params(n_levels=24)
-    layout, _ = oracle.grid_layout(1920, 1080, params)
-    vis_all, det_all = 0, 0
-    for f in range(32):
-        T = oracle.integral(host[f])
-        if f in (0, 2, 31):
-            assert det.dump_integral(1920, 1080, frame=f).view(np.uint32).tobytes() == \
-                T.view(np.uint32).tobytes(), f
-        p, s, v = det.dump_grid(frame=f)
-        rp, rs = oracle.eval_grid(T, face_cascade, params)
-        if f in (0, 2, 31):
-            ev = p != -2
-            np.testing.assert_array_equal(p[ev], rp[ev])
-            assert s[ev].view(np.uint32).tobytes() == rs[ev].view(np.uint32).tobytes(), f
-        rv, _ = oracle.walk_grid(rp, rs, layout, face_cascade.n_stages, params.stride_score)
-        np.testing.assert_array_equal(v, rv)
-        ref, nv = oracle.detect(T, face_cascade, params)
-        assert nv == int(rv.sum())
-        mine = got[got["frame"] == f]
-        assert _det_set(mine) == _det_set(ref), f
-        vis_all += nv
-        det_all += len(ref)
-    assert det.info("visited") == vis_all
-    assert int(counts[0].item()) == det_all
-    det.set_stream(None)
+    _bench_form_exact(sc, oracle, face_cascade, FACE_CFG, 1920, 1080, 32, sc.ScanParams(n_levels=24),
+                      oracle.Params(n_levels=24),
+                      {"fused_frames": 30, "chain_waves": 16, "chain_subq": 1, "column_pass": 1}, (0, 2, 31))
+
+
+def test_c4_bench_form_exact(sc, oracle, face_cascade):
+    """C4 exactly as bench.py measures it: 8 device-resident 4K frames x 32
+    levels (l up to 1343, sums past 2^24) in ONE call with the calibrated
+    model: one frame integrated before the chain kernel (a 4K table is larger
+    than 128 MiB), the column walks of the other 7 inside it, 10 waves.
+    Tables and per-window bits of frames 0, 1 and 7; visited sets and
+    detections of all 8."""
+    _bench_form_exact(sc, oracle, face_cascade, FACE_CFG, 3840, 2160, 8, sc.ScanParams(n_levels=32),
+                      oracle.Params(n_levels=32),
+                      {"fused_frames": 7, "chain_waves": 10, "chain_subq": 1}, (0, 1, 7))
+
+
+def test_c5_bench_form_exact(sc, oracle, ped_cascade):
+    """C5 exactly as bench.py measures it: 32 device-resident 1080p frames x
+    23 levels of the 64 x 128 pedestrian cascade (windows l x 2l) in ONE call:
+    30 frames integrated inside the 12-wave chain kernel (the pedestrian
+    model's LDS copy leaves no room for 16 waves).  Tables and per-window bits
+    of frames 0, 2 and 31; visited sets and detections of all 32."""
+    _bench_form_exact(sc, oracle, ped_cascade, PED_CFG, 1920, 1080, 32, sc.ScanParams.pedestrian(n_levels=23),
+                      oracle.Params(base_len=64, aspect_h=2, n_levels=23),
+                      {"fused_frames": 30, "chain_waves": 12, "chain_subq": 1, "column_pass": 1}, (0, 2, 31))
 
 
 def test_one_frame_launch_uses_four_subqueues(sc, oracle, face_cascade):
