@@ -123,6 +123,12 @@ void l2sim_set_cell_bytes(int b) { g_cell_bytes = b; }
  * from it: the tasks in flight on one CU are neighbouring rows */
 static int g_cu_chunk = 0;
 void l2sim_set_cu_chunk(int c) { g_cu_chunk = c; }
+/* pair = 1: two lanes per item, lane h loading channel half h, so one wave
+ * load covers corner slot m of 32 items in both halves (10 loads per
+ * iteration of 32 items instead of 20 per 64); meant with the interleaved
+ * 32-B cell layout, where an item's two halves share a line */
+static int g_pair = 0;
+void l2sim_set_pair(int p) { g_pair = p; }
 int l2sim_run(const Geom *g, int n_tasks, const int64_t *it_off, const int32_t *items,
               const int32_t *rects, const float *scale, int conc, int cus, int l1_lines,
               int l2_lines, const int32_t *xcd_of_task, const int32_t *grp_of_level, int n_groups,
@@ -176,7 +182,8 @@ int l2sim_run(const Geom *g, int n_tasks, const int64_t *it_off, const int32_t *
                 int t = act[s];
                 if (t < 0) continue;
                 const int64_t end = it_off[t + 1];
-                const int n = (int)((end - pos[s]) < 64 ? (end - pos[s]) : 64);
+                const int per = g_pair ? 32 : 64;
+                const int n = (int)((end - pos[s]) < per ? (end - pos[s]) : per);
                 const int cu = s % cus;
                 int grp = 0;
                 for (int i = 0; i < n; i++) {
@@ -189,11 +196,13 @@ int l2sim_run(const Geom *g, int n_tasks, const int64_t *it_off, const int32_t *
                         item_cells(g, rects + 4 * it[3], scale[it[0]], it[1], g->step * it[2], cells[i]);
                     }
                 }
-                /* 20 wave-level loads; distinct lines per load = L1 accesses */
-                for (int m = 0; m < 20; m++) {
+                /* 20 wave-level loads (10 in pair mode); distinct lines per load = L1 accesses */
+                for (int m = 0; m < (g_pair ? 10 : 20); m++) {
                     int nl = 0;
-                    for (int i = 0; i < 2 * n; i++) {
-                        const uint64_t b0 = (uint64_t)(cells[i >> 1][m] * g_cell_bytes);
+                    for (int i = 0; i < 2 * n * (g_pair ? 2 : 1); i++) {
+                        /* pair: entries (item, half, first/last byte); else (item, first/last byte) */
+                        const int it_i = g_pair ? i >> 2 : i >> 1, mm = g_pair ? m + 10 * ((i >> 1) & 1) : m;
+                        const uint64_t b0 = (uint64_t)(cells[it_i][mm] * g_cell_bytes);
                         const uint64_t ln = (i & 1) ? (b0 + g_cell_bytes - 1) >> 7 : b0 >> 7;
                         int seen = 0;
                         for (int u = 0; u < nl; u++)

@@ -125,6 +125,7 @@ def main():
     ap.add_argument("--alt-from", type=int, default=-1,
                     help="stages >= this read a second table copy in --alt-layout (hybrid layouts)")
     ap.add_argument("--alt-layout", default="inter", choices=("split", "inter", "pix"))
+    ap.add_argument("--pair", action="store_true", help="two lanes per item, one per channel half (use with --layout inter)")
     ap.add_argument("--cu-chunk", type=int, default=0,
                     help="a CU takes this many consecutive queue tasks at a time (per-workgroup sub-queue)")
     ap.add_argument("--big-slots", type=int, default=-1,
@@ -171,6 +172,7 @@ def main():
     L = lib()
     L.l2sim_set_cell_bytes(a.cell_bytes)
     L.l2sim_set_cu_chunk(a.cu_chunk)
+    L.l2sim_set_pair(1 if a.pair else 0)
     L.l2sim_run(ctypes.byref(g), len(it_off) - 1, it_off.ctypes.data, items.ctypes.data, rec.ctypes.data,
                 scale.ctypes.data, a.conc, 32, 256, int(a.l2_mib * 8192), xcd.ctypes.data, grp.ctypes.data, ng,
                 stats.ctypes.data, a.big_slots, gw.ctypes.data if gw is not None else None,
