@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round 5 soak: the parity soak (soak.py), then the chain kernel's per-launch
+# Round 5 soak: the parity soak (tests/soak_parity.py), then the chain kernel's per-launch
 # durations over 300 C2 steps and 2000 one-frame steps (rocprofv3 kernel
 # trace): tail latency of the persistent kernel on the kept build.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; O=$R/gpurun_out/soak; mkdir -p $O
-timeout -k 10 300 python3 -u profiles/r5/soak/soak.py --cases 8 --seed 1 > $O/soak_smoke.log 2>&1 || { tail -20 $O/soak_smoke.log; exit 1; }
+timeout -k 10 300 python3 -u tests/soak_parity.py --cases 8 --seed 1 > $O/soak_smoke.log 2>&1 || { tail -20 $O/soak_smoke.log; exit 1; }
 tail -1 $O/soak_smoke.log | cut -c1-300
-timeout -k 10 1000 python3 -u profiles/r5/soak/soak.py --cases 300 --seed 9000 --out $O/soak.json > $O/soak.log 2>&1; rc=$?
+timeout -k 10 1000 python3 -u tests/soak_parity.py --cases 300 --seed 9000 --out $O/soak.json > $O/soak.log 2>&1; rc=$?
 tail -3 $O/soak.log | cut -c1-400
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 1
 ( cd /tmp && export TMPDIR=/tmp &&

@@ -6,7 +6,9 @@ change a bit (chain waves, dequeue sub-queues, integral fusion and prebuilt
 frames).  Every frame: visited count, visited set and detections (f64 scores);
 every 4th case also the integral table and per-window stage / score bits.
 
-    python profiles/r5/soak/soak.py [--cases 300] [--seed 9000]
+    python tests/soak_parity.py [--cases 300] [--seed 9000] [--out F]
+
+(Not collected by pytest: a GPU soak run by hand; results in profiles/r5/soak/.)
 """
 import argparse
 import json
@@ -16,7 +18,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
