@@ -199,7 +199,7 @@ int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, 
 #define SC_INFO_FUSED_FRAMES 6  /* frames of the last call whose integral      */
                                 /* column walks ran inside the chain kernel    */
 #define SC_INFO_CHAIN_WAVES 7   /* waves per workgroup of the last chain-kernel */
-                                /* launch (12 or 16; 0: none yet)              */
+                                /* launch (8, 10, 12, 14 or 16; 0: none yet)   */
 #define SC_INFO_COLUMN_PASS 8   /* the last call's integral column pass for the */
                                 /* frames built outside the chain kernel:      */
                                 /* 1 two-pass (rowcarry R + colsum), 2 colstrip,*/
@@ -246,8 +246,8 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
 #define SC_OPT_CHAIN_WAVES 17 /* chain kernel waves per CU: 0 auto (16 when the  */
                               /* model and their scratch fit the LDS, a        */
                               /* frame's table is <= 128 MiB and the launch    */
-                              /* has 2+ frames; 10 for tables > 128 MiB),      */
-                              /* 8, 10, 12, 14, 16                             */
+                              /* has 2+ frames; 10 for tables > 128 MiB with   */
+                              /* 2+ frames; else 12), or 8, 10, 12, 14, 16     */
 #define SC_OPT_INTEGRAL_FUSE 18 /* integral column walks inside the chain      */
                               /* kernel: 0 auto (from 4 frames per launch),   */
                               /* 1 never, 2 whenever a launch has 2+ frames    */

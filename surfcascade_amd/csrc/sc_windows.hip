@@ -1418,7 +1418,7 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hi
     if (c.chain_waves == 8 || c.chain_waves == 10 || c.chain_waves == 12 ||
         ((c.chain_waves == 14 || c.chain_waves == 16) &&
          model_lds_bytes(a.K, false) + scratch(c.chain_waves) <= kLds))
-        nw = c.chain_waves;  // SC_OPT_CHAIN_WAVES (10 / 14: A/B only)
+        nw = c.chain_waves;  // SC_OPT_CHAIN_WAVES (8 / 14: A/B only)
     bool lw = model_lds_bytes(a.K, true) + scratch(nw) <= kLds;
     if (c.lds_weights >= 0) lw = lw && c.lds_weights != 0;  // SC_OPT_LDS_WEIGHTS
     const size_t lds = model_lds_bytes(a.K, lw) + scratch(nw);
