@@ -6,7 +6,7 @@ set -e
 S=gpurun_out/r5final; D=profiles/r5/final
 mkdir -p $D
 cp $S/bench.json $S/bench_C1.json $S/bench_C4.json $S/bench_C5.json $D/
-cp $S/pytest.log $S/smoke.log $D/
+cp $S/pytest.log $S/smoke.log $S/legs.json $D/
 cp $S/trace/trace_kernel_stats.csv $D/rocprof_kernel_stats_c2.csv
 cp $S/trace_b1/trace_kernel_stats.csv $D/rocprof_kernel_stats_b1.csv
 for c in C2 C4 C5; do
