@@ -70,14 +70,15 @@ def test_shard_range_covers_all():
         assert seen == list(range(n))
 
 
-@pytest.mark.parametrize("world,tight,own_b", [(2, False, False), (2, True, False), (2, False, True)])
+@pytest.mark.parametrize("world,tight,own_b", [(2, False, False), (2, True, False), (2, False, True),
+                                                 (4, False, True)])
 def test_gloo_gather_equals_single_process(oracle, world, tight, own_b):
     from surfcascade_amd import RECORD_DTYPE, synth
     from surfcascade_amd.dist import merge_records
     n_frames = 5
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = 29500 + os.getpid() % 1000 + (7 if tight else 0) + (13 if own_b else 0)
+    port = 29500 + os.getpid() % 1000 + (7 if tight else 0) + (13 if own_b else 0) + (29 if world > 2 else 0)
     procs = [ctx.Process(target=_worker, args=(r, world, port, n_frames, q, tight, own_b))
              for r in range(world)]
     for p in procs:
