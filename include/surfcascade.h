@@ -207,7 +207,7 @@ int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, 
 #define SC_INFO_SPEC_ROUNDS 9   /* speculative evaluation rounds of the last    */
                                 /* chain launch (one-frame launches only)      */
 #define SC_INFO_CHAIN_SUBQ 10   /* dequeue sub-queues per XCD of the last chain  */
-                                /* launch (4 one-frame launches, 1 batches)    */
+                                /* launch (8 one-frame launches, 1 batches)    */
 int sc_detector_info(sc_detector *d, int what, int64_t *value);
 
 /* ---- tuning and test options ---------------------------------------------
@@ -261,7 +261,7 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
                               /* the test-hook build (lib/testhooks) accepts */
                               /* a value other than -1                       */
 #define SC_OPT_CHAIN_SUBQ 21  /* chain kernel dequeue counters per XCD queue: */
-                              /* 0 auto (4 for a one-frame launch, else 1),    */
+                              /* 0 auto (8 for a one-frame launch, else 1),    */
                               /* or 1..8                                       */
 #define SC_OPT_TEST_DROP_WALK 22 /* test only (-1 off): the fused column walk  */
                               /* `value` of every launch does not count itself */

@@ -850,10 +850,11 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             wc.frame0 = f0;
             wc.drop_task1 = d->opt.drop_handoff + 1;  // SC_OPT_TEST_DROP_HANDOFF (0: none)
             wc.drop_walk1 = d->opt.drop_walk + 1;     // SC_OPT_TEST_DROP_WALK (0: none)
-            // dequeue sub-queues (SC_OPT_CHAIN_SUBQ): 4 for a one-frame launch
-            // (chain kernel 0.589 vs 0.606 ms per 1080p frame), 1 for batches
-            // (C2 with 4: 17.0 vs 13.6 ms; profiles/r4/subq)
-            wc.subq = d->opt.chain_subq ? d->opt.chain_subq : (nc == 1 ? 4 : 1);
+            // dequeue sub-queues (SC_OPT_CHAIN_SUBQ): 8 for a one-frame launch
+            // (chain kernel 0.573 vs 0.582 ms with 4 per 1080p frame,
+            // profiles/r5/l/split; 4 vs 1: 0.589 vs 0.606, profiles/r4/subq),
+            // 1 for batches (C2 with 4: 17.0 vs 13.6 ms)
+            wc.subq = d->opt.chain_subq ? d->opt.chain_subq : (nc == 1 ? 8 : 1);
             d->last_subq = wc.subq;
             wc.nseg = segs_for(nc);
             d->last_nseg = wc.nseg;

@@ -40,7 +40,7 @@ constexpr int kMaxSubQ = 8;       // chain kernel: dequeue counters per XCD queu
 constexpr int kQueueWords = kXcds * kMaxSubQ * kQueueStride;  // the queue buffer
 // chain kernel: segments per row, chosen per launch (WalkArgs::nseg, a power
 // of 2 dividing kXcds); XCD x serves segment x / (kXcds / nseg) and, of that
-// segment, the rows of class x % (kXcds / nseg)
+// segment, part x % (kXcds / nseg) of the row list (contiguous parts)
 
 struct TableGeom {
     int W, H, step;
@@ -200,7 +200,7 @@ struct WalkArgs {
     int frame0;      // chain kernel: first frame of this launch (record frame index)
     int nseg;        // chain kernel: segments per row (8; 4 for one-frame launches)
     int seg_shift;   // chain kernel: log2(kXcds / nseg)
-    int subq;        // chain kernel: dequeue counters per XCD queue (1..kMaxSubQ; 4 for one-frame launches)
+    int subq;        // chain kernel: dequeue counters per XCD queue (1..kMaxSubQ; 8 for one-frame launches)
     unsigned long long *prof;  // chain kernel, SC_PROF_CHAIN builds: phase cycle totals (or null)
     // Fused integral (chain kernel): colstrip's column walks of frames
     // [int_f0, n_frames) of this launch run inside the chain kernel as a

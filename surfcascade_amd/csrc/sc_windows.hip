@@ -806,14 +806,15 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     const int S = a.n_stages, cs = g.cs;
     const int n_tasks = w.n_rows * a.n_frames;  // per segment queue, in row order
     const unsigned long long kEven = 0x5555555555555555ull;
-    // queue of XCD q: segment q of every row, in row order, dealt through
-    // nsq counters on separate lines (sub-queue u: tasks u, u + nsq, ...).
-    // A drained sub-queue sends the wave on to the next one, then to the
-    // other XCDs' queues.  nsq is per launch (WalkArgs::subq): one-frame
-    // launches use 4 (their ~400 waves per XCD otherwise serialise on one
-    // atomic word's line: chain kernel 0.589 vs 0.606 ms, profiles/r4/subq),
-    // batches 1 (sub-queues deal the row blocks out of order and cost their
-    // L2 locality: C2 +25 %)
+    // queue of XCD q: its part of segment q >> sh of every row, in row order,
+    // dealt through nsq counters on separate lines (sub-queue u: tasks u,
+    // u + nsq, ...).  A drained sub-queue sends the wave on to the next one,
+    // then to the other XCDs' queues.  nsq is per launch (WalkArgs::subq):
+    // one-frame launches use 8 (their ~400 waves per XCD otherwise serialise
+    // on one atomic word's line: chain kernel 0.589 vs 0.606 ms with 4,
+    // profiles/r4/subq; 0.573 vs 0.582 with 8 over contiguous parts,
+    // profiles/r5/l/split), batches 1 (sub-queues deal the row blocks out of
+    // order and cost their L2 locality: C2 +25 %)
     const int nsg = w.nseg, sh = w.seg_shift;  // segments per row; XCDs per segment = 1 << sh
     const int nsq = w.subq;
     int q = (int)xcc_id(), empty = 0;
@@ -895,13 +896,21 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     // own queue.  s/2 measured best of 0, s/2, s, 3s/2, 2s, 4s (-1.0 % at 32
     // frames per launch, -8.5 % at one frame; profiles/r2/fill).
     int pre = SC_FILL_K * (q >> sh) / SC_FILL_DEN;
+    // queue position k of XCD sub-index q0 (of the 1 << sh XCDs serving a
+    // segment) -> task k of part q0 of the row list: the XCDs sharing a
+    // segment (one-frame launches: 2) take contiguous parts, so an XCD's tasks
+    // in flight are neighbouring rows; dealt alternately (task (k << sh) + q0)
+    // they spanned twice the rows and the one-frame chain kernel took
+    // 0.5875 vs 0.5823 ms, 0.573 with 8 sub-queues (profiles/r5/l/split)
+    const int psz = (n_tasks + (1 << sh) - 1) >> sh;
+    auto task_of = [&](int k, int q0) -> int { return k < psz ? q0 * psz + k : n_tasks; };
     auto dequeue = [&](int &t, int &qq, int2 &rd) -> bool {
         while (pre > 0) {
             pre--;
             const int q0 = q & ((1 << sh) - 1);  // an XCD of segment 0
             int v = 0;
             if (lead_lane()) v = atomicAdd(&a.queues[(q0 * kMaxSubQ + u) * kQueueStride], 1);
-            v = ((__builtin_amdgcn_readfirstlane(v) * nsq + u) << sh) + q0;
+            v = task_of(__builtin_amdgcn_readfirstlane(v) * nsq + u, q0);
             if (v < n_tasks) {
                 t = v;
                 qq = 0;
@@ -913,7 +922,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         while (!drained) {
             int v = 0;
             if (lead_lane()) v = atomicAdd(&a.queues[(q * kMaxSubQ + u) * kQueueStride], 1);
-            v = ((__builtin_amdgcn_readfirstlane(v) * nsq + u) << sh) + (q & ((1 << sh) - 1));
+            v = task_of(__builtin_amdgcn_readfirstlane(v) * nsq + u, q & ((1 << sh) - 1));
             if (v < n_tasks) {
                 t = v;
                 qq = q >> sh;  // the segment

@@ -333,10 +333,11 @@ def test_c5_bench_form_exact(sc, oracle, ped_cascade):
                       {"fused_frames": 30, "chain_waves": 12, "chain_subq": 1, "column_pass": 1}, (0, 2, 31))
 
 
-def test_one_frame_launch_uses_four_subqueues(sc, oracle, face_cascade):
-    """One-frame launches deal their tasks through 4 dequeue sub-queues per
-    XCD (SC_INFO_CHAIN_SUBQ), batches through one; results are the oracle's
-    at every sub-queue count (SC_OPT_CHAIN_SUBQ)."""
+def test_one_frame_launch_uses_eight_subqueues(sc, oracle, face_cascade):
+    """One-frame launches deal their tasks through 8 dequeue sub-queues per
+    XCD (SC_INFO_CHAIN_SUBQ), each of the two XCDs of a segment over its own
+    contiguous part of the row list; batches through one; results are the
+    oracle's at every sub-queue count (SC_OPT_CHAIN_SUBQ)."""
     img = _frame(1920, 1080, 1234)
     params = oracle.Params(n_levels=24)
     T = oracle.integral(img)
@@ -346,7 +347,7 @@ def test_one_frame_launch_uses_four_subqueues(sc, oracle, face_cascade):
         det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=24)).set_options(chain_subq=q)
         det.set_debug(True)
         wins = det.detect(img)
-        assert det.info("chain_subq") == (4 if q == 0 else q)
+        assert det.info("chain_subq") == (8 if q == 0 else q)
         p, s, _v = det.dump_grid()
         ev = p != -2
         np.testing.assert_array_equal(p[ev], rp[ev])
