@@ -44,12 +44,13 @@ N_CUS = 256
 CSRC = os.path.join(ROOT, "surfcascade_amd", "csrc")
 
 
-def source_build_id(extra=""):
+def source_build_id(extra="", arch="gfx950", san=""):
     """The build id the Makefile gives a library built from the current tree
-    with EXTRA flags `extra` (sc_build_info "build_id"): sha256 over every
-    csrc/*.hip, *.hpp, *.cpp (sorted), the Makefile, include/surfcascade.h and
-    the flags string -- kernels, the launch schedule in sc_api.cpp and every
-    -D knob alike."""
+    with EXTRA flags `extra`, ARCH `arch` and SAN `san` (sc_build_info
+    "build_id"): sha256 over every csrc/*.hip, *.hpp, *.cpp (sorted), the
+    Makefile, include/surfcascade.h and "extra|arch|san" -- kernels, the launch
+    schedule in sc_api.cpp, every -D knob, the target and a sanitizer build
+    alike."""
     import hashlib
     names = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp", ".cpp")))
     h = hashlib.sha256()
@@ -57,7 +58,7 @@ def source_build_id(extra=""):
                                                             os.path.join(ROOT, "include", "surfcascade.h")]:
         with open(path, "rb") as fh:
             h.update(fh.read())
-    h.update(extra.encode())
+    h.update(("%s|%s|%s" % (extra, arch, san)).encode())
     return h.hexdigest()[:16]
 
 

@@ -333,7 +333,8 @@ int sc_fast_nms(const sc_scored_rect *in, int n, double overlap_th,
  * (luma, as libjpeg's JCS_GRAYSCALE output: JDCT_ISLOW inverse DCT).  Writes
  * a w x h plane with row stride w.  *w / *h are set even when the buffer is
  * too small (SC_ERR_CAPACITY), so a NULL / 0 call sizes the buffer.
- * SC_ERR_PARSE: not a JPEG, or an unsupported coding process. */
+ * SC_ERR_PARSE: not a JPEG, an unsupported coding process, a corrupt
+ * Huffman table, or more than 2^28 pixels (twice what a detector accepts). */
 int sc_decode_jpeg_gray(const uint8_t *data, size_t len, uint8_t *out,
                         size_t cap, int *w, int *h);
 int sc_imread_gray(const char *path, uint8_t *out, size_t cap, int *w,

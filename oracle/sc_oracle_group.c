@@ -90,7 +90,7 @@ static int round_d(double v) { return (int)lrint(v); }
 int sco_group_rectangles(const sco_rect *in, int n, int group_threshold, double eps,
                          sco_rect *out) {
     if (group_threshold <= 0 || n == 0) {
-        memcpy(out, in, sizeof(sco_rect) * (size_t)n);
+        if (n > 0) memcpy(out, in, sizeof(sco_rect) * (size_t)n);
         return n;
     }
     int *labels = (int *)malloc(sizeof(int) * (size_t)n);

@@ -136,7 +136,7 @@ struct sc_detector {
         int integral_pre = 0;            // fused: frames integrated before the chain kernel (0: 2)
         int drop_handoff = -1;           // test only: task whose segment-0 hand-off is dropped (watchdog)
         int drop_walk = -1;              // test only: fused column walk whose completion count is dropped
-        int chain_subq = 0;              // chain kernel dequeue sub-queues per XCD (0 auto: 4 one frame, else 1)
+        int chain_subq = 0;              // chain kernel dequeue sub-queues per XCD (0 auto: 8 one frame, else 1)
     } opt;
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
@@ -902,7 +902,7 @@ void check_chain(sc_detector *d) {
         if (!err) err = 1;
     }
     if (err) {
-        throw Error{SC_ERR_DEVICE, "chain kernel: " + std::to_string(err) + " segment hand-off(s) timed out"};
+        throw Error{SC_ERR_DEVICE, "chain kernel: " + std::to_string(err) + " segment hand-off or table wait(s) timed out"};
     }
     if (d->d_prof.p) {
         unsigned long long pc[16];

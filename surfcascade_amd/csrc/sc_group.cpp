@@ -27,12 +27,19 @@ namespace sc {
 
 namespace {
 
+// Integer sums and differences of rectangle coordinates in 64 bits: OpenCV
+// computes them in int, which gives the same values for every rectangle
+// whose coordinates do not overflow (all a detector emits) and undefined
+// behaviour otherwise; the 64-bit form is defined for any int32 input
+// (tests/test_fuzz_parsers.py runs it under UBSan).
+typedef long long i64;
+
 // SimilarRects::operator() (OpenCV cascadedetect.hpp)
 inline bool similar(const sc_scored_rect &a, const sc_scored_rect &b, double eps) {
-    const double delta = eps * (std::min(a.width, b.width) + std::min(a.height, b.height)) * 0.5;
-    return std::abs(a.x - b.x) <= delta && std::abs(a.y - b.y) <= delta &&
-           std::abs(a.x + a.width - b.x - b.width) <= delta &&
-           std::abs(a.y + a.height - b.y - b.height) <= delta;
+    const double delta = eps * (double)((i64)std::min(a.width, b.width) + std::min(a.height, b.height)) * 0.5;
+    return (double)std::llabs((i64)a.x - b.x) <= delta && (double)std::llabs((i64)a.y - b.y) <= delta &&
+           (double)std::llabs((i64)a.x + a.width - b.x - b.width) <= delta &&
+           (double)std::llabs((i64)a.y + a.height - b.y - b.height) <= delta;
 }
 
 struct UnionFind {
@@ -67,10 +74,10 @@ std::vector<sc_scored_rect> group_rectangles(const sc_scored_rect *in, int n, in
     UnionFind uf(n);
     for (int s = 0; s < n; s++) {
         const sc_scored_rect &a = in[ord[s]];
-        const double reach = eps * (a.width + a.height) * 0.5;  // delta <= this for any partner
+        const double reach = eps * (double)((i64)a.width + a.height) * 0.5;  // delta <= this for any partner
         for (int t = s + 1; t < n; t++) {
             const sc_scored_rect &b = in[ord[t]];
-            if (b.x - a.x > reach) break;
+            if ((double)((i64)b.x - a.x) > reach) break;
             if (similar(a, b, eps)) uf.unite(ord[s], ord[t]);
         }
     }
@@ -115,10 +122,10 @@ std::vector<sc_scored_rect> group_rectangles(const sc_scored_rect *in, int n, in
             const int n2 = cnt[j];
             if (j == i || n2 <= group_threshold) continue;
             const sc_scored_rect &r2 = rr[j];
-            const int dx = (int)std::lrint(r2.width * eps), dy = (int)std::lrint(r2.height * eps);
+            const i64 dx = (int)std::lrint(r2.width * eps), dy = (int)std::lrint(r2.height * eps);
             inside = r1.x >= r2.x - dx && r1.y >= r2.y - dy &&
-                     r1.x + r1.width <= r2.x + r2.width + dx &&
-                     r1.y + r1.height <= r2.y + r2.height + dy && (n2 > std::max(3, n1) || n1 < 3);
+                     (i64)r1.x + r1.width <= (i64)r2.x + r2.width + dx &&
+                     (i64)r1.y + r1.height <= (i64)r2.y + r2.height + dy && (n2 > std::max(3, n1) || n1 < 3);
         }
         if (!inside) out.push_back(r1);
     }
@@ -161,7 +168,7 @@ std::vector<sc_scored_rect> fast_nms(const sc_scored_rect *in, int n, double ove
         }
     for (int i = 0; i < n; i++) {
         const sc_scored_rect &r = in[idx[i]];
-        inv[idx[i]] = 1.0f / (float)((r.width + 1) * (r.height + 1));
+        inv[idx[i]] = 1.0f / (float)(((i64)r.width + 1) * ((i64)r.height + 1));
     }
     auto sort_stable = [&](int cnt) {  // :290-313, returns the new count
         int i = 0, j = 0;
@@ -189,16 +196,16 @@ std::vector<sc_scored_rect> fast_nms(const sc_scored_rect *in, int n, double ove
     while (count > 0) {
         const int tmp = count - 1, last = idx[tmp];
         picked.push_back(in[last]);
-        const int x0 = in[last].x, y0 = in[last].y;
-        const int x1 = in[last].x + in[last].width, y1 = in[last].y + in[last].height;
+        const i64 x0 = in[last].x, y0 = in[last].y;
+        const i64 x1 = x0 + in[last].width, y1 = y0 + in[last].height;
         idx[tmp] = -1;
         for (int i = tmp - 1; i != -1; i--) {
             const sc_scored_rect &r = in[idx[i]];
-            int tx0 = std::max(x0, r.x), ty0 = std::max(y0, r.y);
-            const int tx1 = std::min(x1, r.x + r.width), ty1 = std::min(y1, r.y + r.height);
+            i64 tx0 = std::max<i64>(x0, r.x), ty0 = std::max<i64>(y0, r.y);
+            const i64 tx1 = std::min<i64>(x1, (i64)r.x + r.width), ty1 = std::min<i64>(y1, (i64)r.y + r.height);
             tx0 = tx1 - tx0 + 1;
             ty0 = ty1 - ty0 + 1;
-            if (tx0 > 0 && ty0 > 0 && (double)((float)(tx0 * ty0) * inv[idx[i]]) > overlap_th)
+            if (tx0 > 0 && ty0 > 0 && (double)((float)((double)tx0 * (double)ty0) * inv[idx[i]]) > overlap_th)
                 idx[i] = -1;
         }
         count = sort_stable(count);

@@ -38,6 +38,8 @@ const int kZigzag[80] = {
     29, 22, 15, 23, 30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54,
     47, 55, 62, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
 
+constexpr long long kMaxPixels = 1ll << 28;
+
 struct Fail {
     std::string msg;
 };
@@ -131,7 +133,7 @@ struct Bits {
         if (hit_marker && marker == 0xD0 + expect) {
             // p points at FF of the marker
             while (p < end && *p != 0xFF) p++;
-            p += 2;
+            p = end - p > 2 ? p + 2 : end;
             hit_marker = false;
         }
         // a missing / wrong RSTn: continue (libjpeg resyncs; corrupt input)
@@ -163,7 +165,12 @@ constexpr int32_t F0_298 = 2446, F0_390 = 3196, F0_541 = 4433, F0_765 = 6270, F0
                   F1_175 = 9633, F1_501 = 12299, F1_847 = 15137, F1_961 = 16069, F2_053 = 16819,
                   F2_562 = 20995, F3_072 = 25172;
 
-inline int32_t descale(int32_t x, int n) { return (x + (1 << (n - 1))) >> n; }
+// The IDCT's products and sums in 32-bit two's-complement arithmetic that
+// wraps (unsigned ops, then an arithmetic shift of the signed value): IJG's
+// INT32 is `long`, 32 bits on the reference's Win64 build, where corrupt
+// coefficients overflow silently; the same bits here, with no signed overflow.
+typedef uint32_t u32;
+inline int32_t descale(u32 x, int n) { return (int32_t)(x + (1u << (n - 1))) >> n; }
 
 // post-IDCT range limit (jdmaster.c prepare_range_limit_table, masked by 1023)
 inline uint8_t range_limit(int32_t v) {
@@ -175,34 +182,34 @@ inline uint8_t range_limit(int32_t v) {
 }
 
 void idct_islow(const int16_t *coef, const uint16_t *q, uint8_t *out, int ostride) {
-    int32_t ws[64];
+    u32 ws[64];
     for (int c = 0; c < 8; c++) {  // pass 1: columns
         const int16_t *in = coef + c;
         const uint16_t *qt = q + c;
-        int32_t *w = ws + c;
+        u32 *w = ws + c;
         if (!in[8] && !in[16] && !in[24] && !in[32] && !in[40] && !in[48] && !in[56]) {
-            const int32_t dc = (int32_t)in[0] * qt[0] * (1 << kPass1Bits);
+            const u32 dc = (u32)in[0] * qt[0] * (1u << kPass1Bits);
             for (int r = 0; r < 8; r++) w[8 * r] = dc;
             continue;
         }
-        int32_t z2 = (int32_t)in[16] * qt[16], z3 = (int32_t)in[48] * qt[48];
-        int32_t z1 = (z2 + z3) * F0_541;
-        int32_t tmp2 = z1 + z3 * -F1_847;
-        int32_t tmp3 = z1 + z2 * F0_765;
-        z2 = (int32_t)in[0] * qt[0];
-        z3 = (int32_t)in[32] * qt[32];
-        int32_t tmp0 = (z2 + z3) * (1 << kConstBits);
-        int32_t tmp1 = (z2 - z3) * (1 << kConstBits);
-        const int32_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
-        tmp0 = (int32_t)in[56] * qt[56];
-        tmp1 = (int32_t)in[40] * qt[40];
-        tmp2 = (int32_t)in[24] * qt[24];
-        tmp3 = (int32_t)in[8] * qt[8];
+        u32 z2 = (u32)in[16] * qt[16], z3 = (u32)in[48] * qt[48];
+        u32 z1 = (z2 + z3) * F0_541;
+        u32 tmp2 = z1 + z3 * -F1_847;
+        u32 tmp3 = z1 + z2 * F0_765;
+        z2 = (u32)in[0] * qt[0];
+        z3 = (u32)in[32] * qt[32];
+        u32 tmp0 = (z2 + z3) * (1u << kConstBits);
+        u32 tmp1 = (z2 - z3) * (1u << kConstBits);
+        const u32 tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+        tmp0 = (u32)in[56] * qt[56];
+        tmp1 = (u32)in[40] * qt[40];
+        tmp2 = (u32)in[24] * qt[24];
+        tmp3 = (u32)in[8] * qt[8];
         z1 = tmp0 + tmp3;
         z2 = tmp1 + tmp2;
         z3 = tmp0 + tmp2;
-        int32_t z4 = tmp1 + tmp3;
-        const int32_t z5 = (z3 + z4) * F1_175;
+        u32 z4 = tmp1 + tmp3;
+        const u32 z5 = (z3 + z4) * F1_175;
         tmp0 *= F0_298;
         tmp1 *= F2_053;
         tmp2 *= F3_072;
@@ -228,20 +235,20 @@ void idct_islow(const int16_t *coef, const uint16_t *q, uint8_t *out, int ostrid
         w[32] = descale(tmp13 - tmp0, sh);
     }
     for (int r = 0; r < 8; r++) {  // pass 2: rows
-        const int32_t *w = ws + 8 * r;
+        const u32 *w = ws + 8 * r;
         uint8_t *o = out + (size_t)r * ostride;
         if (!w[1] && !w[2] && !w[3] && !w[4] && !w[5] && !w[6] && !w[7]) {
             const uint8_t v = range_limit(descale(w[0], kPass1Bits + 3));
             for (int c = 0; c < 8; c++) o[c] = v;
             continue;
         }
-        int32_t z2 = w[2], z3 = w[6];
-        int32_t z1 = (z2 + z3) * F0_541;
-        int32_t tmp2 = z1 + z3 * -F1_847;
-        int32_t tmp3 = z1 + z2 * F0_765;
-        int32_t tmp0 = (w[0] + w[4]) * (1 << kConstBits);
-        int32_t tmp1 = (w[0] - w[4]) * (1 << kConstBits);
-        const int32_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+        u32 z2 = w[2], z3 = w[6];
+        u32 z1 = (z2 + z3) * F0_541;
+        u32 tmp2 = z1 + z3 * -F1_847;
+        u32 tmp3 = z1 + z2 * F0_765;
+        u32 tmp0 = (w[0] + w[4]) * (1u << kConstBits);
+        u32 tmp1 = (w[0] - w[4]) * (1u << kConstBits);
+        const u32 tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
         tmp0 = w[7];
         tmp1 = w[5];
         tmp2 = w[3];
@@ -249,8 +256,8 @@ void idct_islow(const int16_t *coef, const uint16_t *q, uint8_t *out, int ostrid
         z1 = tmp0 + tmp3;
         z2 = tmp1 + tmp2;
         z3 = tmp0 + tmp2;
-        int32_t z4 = tmp1 + tmp3;
-        const int32_t z5 = (z3 + z4) * F1_175;
+        u32 z4 = tmp1 + tmp3;
+        const u32 z5 = (z3 + z4) * F1_175;
         tmp0 *= F0_298;
         tmp1 *= F2_053;
         tmp2 *= F3_072;
@@ -325,6 +332,10 @@ struct Decoder {
                 h.valptr[l] = k;
                 h.mincode[l] = code;
                 for (int i = 0; i < counts[l]; i++, k++, code++) {
+                    // more codes of length l than l bits hold (libjpeg
+                    // jdhuff.c: JERR_BAD_HUFF_TABLE); the lookahead fill
+                    // below would index past its 512 entries
+                    if (code >= (1 << l)) throw Fail{"bad Huffman table"};
                     if (l <= 9) {
                         const int sh = 9 - l;
                         for (int f = 0; f < (1 << sh); f++)
@@ -346,6 +357,11 @@ struct Decoder {
         W = u16();
         const int nf = u8();
         if (W <= 0 || H <= 0) throw Fail{"JPEG without dimensions (DNL) is not supported"};
+        // the coefficient plane is allocated from these two header fields:
+        // bound it (twice the largest frame a detector accepts, about 2^27
+        // px: sc_api.cpp's 32-bit table offsets) so a 20-byte file cannot
+        // ask for gigabytes
+        if ((long long)W * H > kMaxPixels) throw Fail{"JPEG larger than 2^28 pixels"};
         if (nf != 1 && nf != 3) throw Fail{"only 1- and 3-component JPEG are supported"};
         comps.resize(nf);
         for (Comp &c : comps) {
@@ -376,7 +392,7 @@ struct Decoder {
         if (!progressive) {
             const int t = decode_huff(b, dc[c.dc_tbl]);
             const int s = t & 15;
-            c.dc_pred += extend(b.get(s), s);
+            c.dc_pred = (int)((unsigned)c.dc_pred + (unsigned)extend(b.get(s), s));  // (wraps as IJG's int)
             if (blk) blk[0] = (int16_t)c.dc_pred;
             const Huff &ha = ac[c.ac_tbl];
             for (int k = 1; k < 64; k++) {
@@ -396,8 +412,8 @@ struct Decoder {
             if (ah == 0) {
                 const int t = decode_huff(b, dc[c.dc_tbl]);
                 const int s = t & 15;
-                c.dc_pred += extend(b.get(s), s);
-                if (blk) blk[0] = (int16_t)(c.dc_pred * (1 << al));
+                c.dc_pred = (int)((unsigned)c.dc_pred + (unsigned)extend(b.get(s), s));
+                if (blk) blk[0] = (int16_t)((unsigned)c.dc_pred << al);  // (IJG's LEFT_SHIFT)
             } else if (b.bit() && blk) {
                 blk[0] = (int16_t)(blk[0] | (1 << al));
             }

@@ -30,10 +30,17 @@ int Cascade::total_weak() const {
 // ---------------------------------------------------------------------------
 namespace {
 
+// Nesting bound of groups / arrays / lists: libconfig's bison parser fails a
+// too-deep file with a parse error when its stack (YYMAXDEPTH 10000 states)
+// runs out; this recursive-descent reader fails it at 1000 levels (a model
+// nests 4 deep) instead of overflowing the thread's stack.
+constexpr int kMaxDepth = 1000;
+
 struct Parser {
     const std::string &s;
     size_t i = 0;
     int line = 1;
+    int depth = 0;
 
     [[noreturn]] void fail(const std::string &what) {
         throw Error{SC_ERR_PARSE, "model.cfg:" + std::to_string(line) + ": " + what};
@@ -170,13 +177,21 @@ struct Parser {
         if (i >= s.size()) fail("value expected");
         CfgValue v;
         char c = s[i];
+        if ((c == '{' || c == '[' || c == '(') && depth >= kMaxDepth) fail("nested too deeply");
+        struct Nest {  // depth of the aggregate being read (restored on throw too)
+            int &d;
+            explicit Nest(int &x) : d(++x) {}
+            ~Nest() { d--; }
+        };
         if (c == '{') {
+            Nest nest(depth);
             i++;
             v.type = CfgValue::Group;
             settings(v, '}');
             return v;
         }
         if (c == '[' || c == '(') {
+            Nest nest(depth);
             char close = c == '[' ? ']' : ')';
             v.type = c == '[' ? CfgValue::Array : CfgValue::List;
             i++;

@@ -34,6 +34,17 @@ CASES = [  # name, (h, w), seed, mode, save kwargs
     ("prog444_q90", (48, 64), 2, "RGB", dict(quality=90, subsampling=0, progressive=True)),
     ("gray_q60_opt", (23, 17), 3, "L", dict(quality=60, optimize=True)),
     ("prog420_q50", (61, 45), 4, "RGB", dict(quality=50, subsampling=2, progressive=True)),
+    # edge cases (also the seed corpus of tests/test_fuzz_parsers.py): 1-px
+    # images, 1-px-wide strips, 4:2:2, restart intervals per MCU / per MCU row
+    # in sequential and progressive scans
+    ("tiny1_gray", (1, 1), 5, "L", dict(quality=90)),
+    ("tiny1_rgb", (1, 1), 6, "RGB", dict(quality=90, subsampling=2)),
+    ("wide_1x67", (1, 67), 10, "L", dict(quality=50)),
+    ("tall_67x1_444", (67, 1), 11, "RGB", dict(quality=95, subsampling=0)),
+    ("rst1_422", (20, 33), 7, "RGB", dict(quality=80, subsampling=1, restart_marker_blocks=1)),
+    ("rstrow_prog420", (29, 41), 8, "RGB", dict(quality=70, subsampling=2, progressive=True,
+                                                 restart_marker_rows=1)),
+    ("rst3_prog_gray", (19, 70), 9, "L", dict(quality=85, progressive=True, restart_marker_blocks=3)),
 ]
 
 

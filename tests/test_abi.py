@@ -113,7 +113,7 @@ def test_product_library_build_info(sc):
     import importlib.util
     info = sc.build_info()
     assert info["arch"] == "gfx950"
-    assert info["flags"] == ""
+    assert info["flags"] == "" and info["sanitizer"] == ""
     assert info["ablation"] is False and info["test_hooks"] is False and info["profiling"] is False
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
     b = importlib.util.module_from_spec(spec)

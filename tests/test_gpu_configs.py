@@ -169,7 +169,7 @@ try:
     det.synchronize()
     print("NOT RAISED")
 except sc.SurfCascadeError as e:
-    print("RAISED", "hand-off" in str(e))
+    print("RAISED", "hand-off or table wait" in str(e))
 det.enqueue_device(frames, recs, counts)
 det.synchronize()                              # reported once, not carried further
 print("CLEAN AFTER")
@@ -220,7 +220,7 @@ try:
     det.synchronize()
     print("NOT RAISED")
 except sc.SurfCascadeError as e:
-    print("RAISED", "hand-off" in str(e))
+    print("RAISED", "hand-off or table wait" in str(e))
 det.enqueue_device(frames, recs, counts)
 det.synchronize()
 print("CLEAN AFTER")

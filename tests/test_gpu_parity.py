@@ -88,6 +88,26 @@ def test_grid_parity_default_levels_odd_size(sc, oracle, face_cascade):
     _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(), oracle.Params())
 
 
+@pytest.mark.parametrize("W,H,n_lv,l_last", [(1920, 1080, 29, 1009), (3840, 2160, 36, 1967)])
+def test_grid_parity_reference_level_count(sc, oracle, face_cascade, W, H, n_lv, l_last):
+    """The scan the reference itself runs on the headline frame sizes: the
+    default ScanParams take the level count from ObjDetector.cpp:174
+    ((int)min(log(W/70)/log(1.1), log(H/70)/log(1.1)) + 1: 29 levels at 1080p,
+    36 at 4K) and l_i = (int)(70 * 1.1^i) (:180), so the widest level is
+    l = 1009 / 1967.  Table, per-window stage / score bits, visited set and
+    detections against the oracle."""
+    img = _frame(W, H, 4242)
+    params = oracle.Params()
+    assert oracle.effective_levels(W, H, params) == n_lv
+    layout, _ = oracle.grid_layout(W, H, params)
+    assert len(layout) == n_lv and layout[-1][1] == l_last and layout[-1][3] > 0
+    dets = []
+    _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(), params, det_out=dets)
+    assert dets[0].info("levels") == n_lv
+    T = dets[0].dump_integral(W, H)
+    assert T.view(np.uint32).tobytes() == oracle.integral(img).view(np.uint32).tobytes()
+
+
 @pytest.mark.parametrize("chunk_min,substrips,band_rows,layout,full", [
     ("1", None, None, None, "1"), ("40", None, "3", "0", "1"), (None, "3", "1", "1", "1"),
     (None, "2", "5", None, "1"), ("1", None, "2", "1", "1"), (None, None, None, "0", None),
@@ -577,6 +597,25 @@ def test_one_frame_column_pass_in_segments(sc, oracle, W, H, amp):
     assert det.info("column_pass") == 3
     T = det.dump_integral(W, H)
     assert T.view(np.uint32).tobytes() == ref.view(np.uint32).tobytes()
+
+
+@pytest.mark.parametrize("kind", ["noise", "checker"])
+@pytest.mark.parametrize("W,H", [(2051, 1000), (4099, 700), (2305, 333)])
+def test_one_frame_merged_integral_odd_wide(sc, oracle, W, H, kind):
+    """The one-frame merged launch (rowcarry4_colblk: row carries plus the
+    exact 32-row column-block sums colseg starts from) at odd widths above
+    2048: its block role walks more than 8 passes of 256 columns, so the
+    running sum crosses chunks, AND the last pass is partial (lanes past W,
+    the byte-wise tail of the dword pixel loads).  ADVICE r5: neither the
+    soak (W <= 900) nor the 4K tests (3840 = 15 x 256) combine the two."""
+    yy, xx = np.mgrid[0:H, 0:W]
+    img = (np.random.default_rng(W + H).integers(0, 256, (H, W)) if kind == "noise"
+           else ((xx + yy) & 1) * 255).astype(np.uint8)
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=1))
+    det.detect(img)
+    assert det.info("column_pass") == 3
+    T = det.dump_integral(W, H)
+    assert T.view(np.uint32).tobytes() == oracle.integral(img).view(np.uint32).tobytes()
 
 
 @pytest.mark.parametrize("layout", ["0", "1"])
