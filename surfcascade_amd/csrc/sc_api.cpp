@@ -36,7 +36,19 @@ struct sc_model {
 namespace {
 
 constexpr int kBandRows = 1;  // grid rows per cascade task (SC_BAND_ROWS overrides)
-constexpr bool kSplitLayout = true;  // table cell format (SC_TABLE_LAYOUT=0/1 overrides)
+constexpr bool kSplitLayout = true;  // table cell format (SC_OPT_TABLE_LAYOUT 1: interleaved)
+#if defined(SC_PAIR) && SC_PAIR
+// the lane-pair item form (sc_device.hpp) runs on interleaved cells: chosen
+// for frame tables above 128 MiB (e.g. 4K), where sparse late-stage items
+// dominate the misses; SC_OPT_TABLE_LAYOUT 1 forces it for any frame
+constexpr bool kPairBigTables = true;
+#ifndef SC_PAIR_MIN_MIB  // (A/B: 0 puts every lazy-grid frame on the lane-pair form)
+#define SC_PAIR_MIN_MIB 128
+#endif
+#else
+#define SC_PAIR_MIN_MIB 128
+constexpr bool kPairBigTables = false;
+#endif
 
 thread_local std::string g_err;
 
@@ -99,6 +111,7 @@ struct Geometry {
     std::vector<sc::LevelInfo> levels;
     std::vector<int2> rows;   // chain kernel task order (rows1: one-frame launches)
     std::vector<int2> rows1;
+    int n_wide = 0;           // SC_WIDECAP builds: the wide levels' rows at the end of `rows`
     std::vector<sc::ProjPatch> proj;
     std::vector<sc::ProjPatch> proj_all;  // miner: every template patch per level
     std::vector<sc::TaskDesc> tasks;
@@ -289,10 +302,12 @@ void build_geometry(sc_detector *d, int W, int H) {
         const int Q = (W + 1 + t.ph - 1) / t.ph;
         t.Qp = (Q + 15) & ~15;
         t.rowp = 2 * t.ph * t.Qp;
-        const bool split = d->opt.table_layout ? false : kSplitLayout;  // SC_OPT_TABLE_LAYOUT
-        t.cs = split ? 1 : 2;
-        t.hs = split ? t.ph * t.Qp : 1;
         t.frame4 = (long long)(H + 1) * t.rowp;
+        const bool split = d->opt.table_layout ? false
+                                               : kSplitLayout && !(kPairBigTables && d->lazy &&
+                                                                   t.frame4 * 16 > ((long long)SC_PAIR_MIN_MIB << 20));
+        t.cs = split ? 1 : 2;  // SC_OPT_TABLE_LAYOUT
+        t.hs = split ? t.ph * t.Qp : 1;
         if ((long long)(H + 1) * t.rowp > (1ll << 28))  // byte offsets within a frame table: u32
             throw Error{SC_ERR_INVALID, "frame too large for 32-bit table offsets"};
         {   // Normalize's operands stay inside the ranges the short sqrt /
@@ -469,6 +484,16 @@ void build_geometry(sc_detector *d, int W, int H) {
         ng.rows1 = d->opt.order_set ? order(ng.rows, d->opt.row_order, d->opt.row_block * ng.step)
                                     : order(ng.rows, 3, 4 * ng.step);
         ng.rows = order(ng.rows, d->opt.row_order, d->opt.row_block * ng.step);
+#if defined(SC_WIDECAP) && SC_WIDECAP
+        // A/B (SC_WIDECAP): the rows of levels with l >= SC_WIDE_L dealt from
+        // a list of their own, each list in the order above
+#ifndef SC_WIDE_L
+#define SC_WIDE_L 690
+#endif
+        auto narrow = std::stable_partition(ng.rows.begin(), ng.rows.end(),
+                                             [&](const int2 &r) { return ng.levels[r.x].l < SC_WIDE_L; });
+        ng.n_wide = (int)(ng.rows.end() - narrow);
+#endif
     }
     d->d_tasks.ensure(std::max<size_t>(ng.tasks.size(), 1));
     if (!ng.tasks.empty())
@@ -855,6 +880,12 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             // profiles/r5/l/split; 4 vs 1: 0.589 vs 0.606, profiles/r4/subq),
             // 1 for batches (C2 with 4: 17.0 vs 13.6 ms)
             wc.subq = d->opt.chain_subq ? d->opt.chain_subq : (nc == 1 ? 8 : 1);
+#if defined(SC_WIDECAP) && SC_WIDECAP
+            if (nc > 1 && wc.subq < sc::kMaxSubQ) {  // (the wide list's counter is sub-queue word kMaxSubQ - 1)
+                wc.n_wide = g.n_wide;
+                wc.wide_cap = SC_WIDECAP;
+            }
+#endif
             d->last_subq = wc.subq;
             wc.nseg = segs_for(nc);
             d->last_nseg = wc.nseg;

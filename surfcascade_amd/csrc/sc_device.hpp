@@ -314,6 +314,133 @@ __device__ __forceinline__ float lr_predict2(const f2 (&fp)[16], const float4 *w
     return (float)prob;
 }
 
+#ifndef SC_PAIR  // 1: lane-pair item form (interleaved 32-B cells); A/B variant, see pair_z32
+#define SC_PAIR 0
+#endif
+
+// ---- lane-pair item form (SC_PAIR) -------------------------------------------
+// One item on two lanes: lane 2i + h holds channel half h (channels 4h..4h+3)
+// of item i, so one 16-B load instruction reads both halves of 32 items'
+// corners from the same 32-B interleaved cells (TableGeom cs 2, hs 1): one
+// line per corner instead of one per half for an isolated window, and 16
+// descriptor floats per lane instead of 32.  Quad q = 2 cell + h of the
+// descriptor (f[4q..4q+3]) lives in lane h; every sequential sum of
+// Normalize and LogisticRegression::Predict runs in both lanes, each term
+// read from the lane that holds it (DPP quad_perm [0,0,2,2] / [1,1,3,3] as
+// the first operand of the add: a + b == b + a bit for bit), so the
+// association is the reference's exactly.
+__device__ __forceinline__ float from_even(float x) {  // the value of lane 2i (quad_perm [0,0,2,2])
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xA0, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float from_odd(float x) {  // the value of lane 2i+1 (quad_perm [1,1,3,3])
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xF5, 0xF, 0xF, true));
+}
+
+// SS = (((eps + c0) + c1) ...) + c7 (:427-433), c_(2 cell + h) in lane h
+__device__ __forceinline__ float ss_pair(const f2 (&fh)[8]) {
+    float c[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {  // every c first: the DPP reads then wait on nothing
+        const f2 a = fh[2 * k] * fh[2 * k], b = fh[2 * k + 1] * fh[2 * k + 1];
+        c[k] = (a.x + a.y) + (b.x + b.y);
+    }
+    float ss = FLT_EPSILON;
+    asm volatile("" : "+v"(ss));  // (in a VGPR: the first add takes the DPP operand too)
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        ss = from_even(c[k]) + ss;
+        ss = from_odd(c[k]) + ss;
+    }
+    return ss;
+}
+
+// One item of the lane-pair form as its projecting lane computed it: the
+// 10 corner offsets (corner_offsets), the origin cell's byte offset, the
+// patch shape and the weak index; of_even / of_odd hand a pair the item of
+// its even / odd lane.
+struct PairItem {
+    int off[10];
+    unsigned base;
+    int shape, gk;
+    template <int CTRL>
+    __device__ __forceinline__ static int bc(int x) {
+        return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, true);
+    }
+    template <int CTRL>
+    __device__ __forceinline__ PairItem of() const {
+        PairItem r;
+#pragma unroll
+        for (int m = 0; m < 10; m++) r.off[m] = bc<CTRL>(off[m]);
+        r.base = (unsigned)bc<CTRL>((int)base);
+        r.shape = bc<CTRL>(shape);
+        r.gk = bc<CTRL>(gk);
+        return r;
+    }
+    __device__ __forceinline__ PairItem of_even() const { return of<0xA0>(); }
+    __device__ __forceinline__ PairItem of_odd() const { return of<0xF5>(); }
+};
+
+// CalcFeature + Normalize + the f32 part of LogisticRegression::Predict
+// (:379-457, LogisticRegression.cpp:46-60) of one item on a lane pair (lane
+// half h: +16 B into each 32-B cell).  Returns z32 = (s0 + s1) + (s2 + s3)
+// in both lanes.  w4: the item's weights (quad q at w4[q]).
+__device__ __forceinline__ float pair_z32(const char *Tb, const PairItem &it, const float4 *w4, int h) {
+#if SC_LOAD_BARRIER
+    __builtin_amdgcn_sched_barrier(0);  // (the next item's loads stay after this one's math)
+#endif
+    const TabView T{Tb, it.base + ((unsigned)h << 4)};
+    float4 cn[10];
+#pragma unroll
+    for (int m = 0; m < 10; m++) cn[m] = T.at(it.off[m]);
+#if SC_LOAD_BARRIER
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    f2 fh[8];
+    half_box(it.shape, cn, fh);
+    const float theta = 0.35355338f;
+    const float t = sqrt_rn(ss_pair(fh)) * theta, nt = -t;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        fh[j].x = __builtin_amdgcn_fmed3f(fh[j].x, nt, t);
+        fh[j].y = __builtin_amdgcn_fmed3f(fh[j].y, nt, t);
+    }
+    const float r = rcp_rn(sqrt_rn(ss_pair(fh)));
+#pragma unroll
+    for (int j = 0; j < 8; j++) fh[j] = fh[j] * f2{r, r};
+    // products as single floats: a DPP operand folds into the add only when
+    // it is a whole 32-bit register (not half of a v_pk result)
+    float p[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const float4 wv = w4[2 * k + h];
+        p[k][0] = wv.x * fh[2 * k].x;
+        p[k][1] = wv.y * fh[2 * k].y;
+        p[k][2] = wv.z * fh[2 * k + 1].x;
+        p[k][3] = wv.w * fh[2 * k + 1].y;
+    }
+    float s[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // lane sums from 0 (LogisticRegression.cpp:51-57)
+#pragma unroll
+    for (int j = 0; j < 4; j++) asm volatile("" : "+v"(s[j]));
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) s[j] = from_even(p[k][j]) + s[j];
+#pragma unroll
+        for (int j = 0; j < 4; j++) s[j] = from_odd(p[k][j]) + s[j];
+    }
+    float z = (s[0] + s[1]) + (s[2] + s[3]);
+    asm volatile("" : "+v"(z));  // computed here: its DPP reads stay next to their adds
+    return z;
+}
+
+// The f64 tail of LogisticRegression::Predict (:61-67) from z32.
+__device__ __forceinline__ float lr_sigmoid(float z32, float wb, double bias) {
+    double prob = (double)z32;
+    prob += (double)wb * bias;
+    prob = 1.0 / (1.0 + exp(-prob));
+    return (float)prob;
+}
+
 // One (window, weak classifier) item.
 template <class P>
 __device__ __forceinline__ float weak_eval(const TabView &T, int half_off, const P &pj, const float4 *w4,

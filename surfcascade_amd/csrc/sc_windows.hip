@@ -393,6 +393,42 @@ __device__ __forceinline__ void eval_windows(const CascadeArgs &a, const Rows &B
                     k = Ol[off + kk];
                 };
                 for (int b2 = 0; b2 < items; b2 += 64) stats.iter(min(64, items - b2));
+#if SC_PAIR
+                // lane-pair form (sc_device.hpp pair_z32) on the interleaved
+                // cells (hs == 1; the split layout keeps the one-lane form):
+                // lane 2i + h decodes and projects item b2 + 32 h + i (the one
+                // whose f64 sigmoid it runs at the end), pass h of the pair
+                // reads those offsets from lane 2i + h (DPP), so each item is
+                // projected once; 32 items per pass on all 64 lanes (lanes past
+                // the items repeat item 0: the cross-lane reads need every lane)
+                if (half_off == 1) {
+                    for (int b2 = 0; b2 < items; b2 += 64) {
+                        const int ln = lane_id<RM>(), h = ln & 1, ii = ln >> 1;
+                        const int t2 = b2 + h * 32 + ii;
+                        int k, i;
+                        decode(t2 < items ? t2 : 0, k, i);
+                        const int gk = off + k;
+                        const unsigned sv = surv[c + i];
+                        const auto pj = B.patch((int)(sv >> 16), (int)(sv & 0xffffu), gk);
+                        PairItem it;
+                        corner_offsets(pj, it.off);
+                        it.base = cell(sv) << 4;
+                        it.shape = pj.shape;
+                        it.gk = gk;
+                        float z[2];
+#pragma unroll
+                        for (int ps = 0; ps < 2; ps++) {
+                            z[ps] = 0.0f;
+                            if (ps == 1 && b2 + 32 >= items) break;  // (wave-uniform)
+                            const PairItem q = ps == 0 ? it.of_even() : it.of_odd();
+                            z[ps] = pair_z32(Tb, q, LW ? Wl + q.gk * 9 : a.w + q.gk * 9, h);
+                        }
+                        if (t2 < items)
+                            P[k * G + i] = LW ? lr_sigmoid(h ? z[1] : z[0], Wl[gk * 9 + 8].x, Bl[gk])
+                                              : lr_sigmoid(h ? z[1] : z[0], a.w[gk * 9 + 8].x, a.bias[gk]);
+                    }
+                } else
+#endif
                 for (int t2 = lane_id<RM>(); t2 < items; t2 += 64) {
                     int k, i;
                     decode(t2, k, i);
@@ -472,7 +508,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
         return make_int2(band * nseg + q * a.n_sub + sub, frame);
     };
     int t = 0;
-    if (lane == 0) t = atomicAdd(&a.queues[q * kQueueStride], 1);
+    if (lead_lane()) t = atomicAdd(&a.queues[q * kQueueStride], 1);
     t = __builtin_amdgcn_readfirstlane(t);
     TaskDesc D{};
     int2 tf = make_int2(0, 0);
@@ -485,7 +521,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
             if (++empty == kXcds) break;
             q = (q + 1) & (kXcds - 1);
             t = 0;
-            if (lane == 0) t = atomicAdd(&a.queues[q * kQueueStride], 1);
+            if (lead_lane()) t = atomicAdd(&a.queues[q * kQueueStride], 1);
             t = __builtin_amdgcn_readfirstlane(t);
             if (t < n_tasks) {
                 tf = task_index(t);
@@ -494,7 +530,7 @@ __global__ __launch_bounds__(kCascadeThreads, SC_CASCADE_MIN_WGS) void cascade_k
             continue;
         }
         int tn = 0;  // prefetch the next task index
-        if (lane == 0) tn = atomicAdd(&a.queues[q * kQueueStride], 1);
+        if (lead_lane()) tn = atomicAdd(&a.queues[q * kQueueStride], 1);
         const int frame = tf.y;
         if (D.nw > 0) {  // (empty strips of narrow rows: nothing to do)
             const char *Tb = reinterpret_cast<const char *>(a.table + (long long)frame * g.frame4);
@@ -628,6 +664,9 @@ __global__ __launch_bounds__(64) void walk_kernel(WalkArgs a) {
 
 #ifndef SC_ABL_EXTRA_RT
 #define SC_ABL_EXTRA_RT 0
+#endif
+#ifndef SC_WIDECAP  // A/B: cap on a CU's task slots holding a wide-level row (0: one row list)
+#define SC_WIDECAP 0
 #endif
 #ifndef SC_CHAIN_SLOTS  // chain kernel: rows (tasks) a wave advances together
 #define SC_CHAIN_SLOTS 2
@@ -785,6 +824,10 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
     // of its walk count and an agent-scope acquire by a wave of this CU)
     int *cu_rdy = reinterpret_cast<int *>(Lv + w.n_levels);
     if (threadIdx.x == 0) *cu_rdy = w.int_walks > 0 ? w.int_f0 : a.n_frames;
+#if SC_WIDECAP
+    int *cu_wide = cu_rdy + 1;  // this CU's slots holding a wide-level row
+    if (threadIdx.x == 0) *cu_wide = 0;
+#endif
     stage_model<LW, kChainThreads>(a, smem, Wl, Bl, Ol, Rl);  // (its barrier covers Lv, cu_rdy)
 
     const int sa = (w.row_max + 63) & ~63, nwords = sa >> 6;  // row_max: widest segment
@@ -804,7 +847,18 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
 
     const TableGeom g = a.g;
     const int S = a.n_stages, cs = g.cs;
+#if SC_WIDECAP
+    // two row lists: the narrow levels' rows [0, nN) and the wide levels'
+    // [nN, n_rows), each dealt in its own order from its own queue; task ids
+    // t < n_tasks narrow (frame t / nN), t >= n_tasks wide
+    const int nW = w.n_wide, nN = w.n_rows - nW;
+    const int n_tasks = nN * a.n_frames, nt_w = nW * a.n_frames;
+    const int pszw = (nt_w + (1 << w.seg_shift) - 1) >> w.seg_shift;
+    int qw = (int)xcc_id(), emptyw = 0;
+    bool wdrained = nt_w == 0, ndrained = false;
+#else
     const int n_tasks = w.n_rows * a.n_frames;  // per segment queue, in row order
+#endif
     const unsigned long long kEven = 0x5555555555555555ull;
     // queue of XCD q: its part of segment q >> sh of every row, in row order,
     // dealt through nsq counters on separate lines (sub-queue u: tasks u,
@@ -914,11 +968,53 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             if (v < n_tasks) {
                 t = v;
                 qq = 0;
+#if SC_WIDECAP
+                rd = row_desc(w.rows, v % nN);
+#else
                 rd = row_desc(w.rows, v % w.n_rows);
+#endif
                 return true;
             }
             pre = 0;
         }
+#if SC_WIDECAP
+        for (;;) {
+            // a wide row while this CU holds fewer than wide_cap (any once the
+            // narrow rows are gone); the count is raised first, returned if
+            // no wide row is taken
+            while (!wdrained) {
+                int old = 0;
+                if (lead_lane()) old = __hip_atomic_fetch_add(cu_wide, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                old = __builtin_amdgcn_readfirstlane(old);
+                bool took = false;
+                if (old < w.wide_cap || ndrained) {
+                    int v = 0;
+                    if (lead_lane()) v = atomicAdd(&a.queues[(qw * kMaxSubQ + kMaxSubQ - 1) * kQueueStride], 1);
+                    v = __builtin_amdgcn_readfirstlane(v);
+                    v = v < pszw ? (qw & ((1 << sh) - 1)) * pszw + v : nt_w;
+                    if (v < nt_w) {
+                        t = n_tasks + v;
+                        qq = qw >> sh;
+                        rd = row_desc(w.rows, nN + v % nW);
+                        took = true;
+                    } else if (++emptyw == kXcds) {
+                        wdrained = true;
+                    } else {
+                        qw = (qw + 1) & (kXcds - 1);
+                    }
+                }
+                if (took) return true;
+                if (lead_lane()) __hip_atomic_fetch_add(cu_wide, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (!(old < w.wide_cap || ndrained) || wdrained) break;
+            }
+            if (ndrained) {
+                drained = wdrained;
+                if (drained) return false;
+                continue;
+            }
+#else
+        {
+#endif
         while (!drained) {
             int v = 0;
             if (lead_lane()) v = atomicAdd(&a.queues[(q * kMaxSubQ + u) * kQueueStride], 1);
@@ -926,7 +1022,11 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             if (v < n_tasks) {
                 t = v;
                 qq = q >> sh;  // the segment
+#if SC_WIDECAP
+                rd = row_desc(w.rows, v % nN);
+#else
                 rd = row_desc(w.rows, v % w.n_rows);
+#endif
                 return true;
             }
             if (++empty == kXcds * nsq) {  // every sub-queue drained
@@ -935,6 +1035,12 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                 u = 0;
                 q = (q + 1) & (kXcds - 1);
             }
+        }
+#if SC_WIDECAP
+            ndrained = true;
+            drained = wdrained;
+            if (drained) return false;
+#endif
         }
         return false;
     };
@@ -960,6 +1066,9 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
 #endif
                 __hip_atomic_store(&w.entry[(long long)tt[sl] * nsg + tq[sl] + 1], pos + 1,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if SC_WIDECAP
+            if (tt[sl] >= n_tasks) __hip_atomic_fetch_add(cu_wide, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
         }
         st[sl] = 0;
     };
@@ -999,7 +1108,11 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     const int nx = Lv[rd.x].nx, nxs = (nx + nsg - 1) / nsg;
                     tt[sl] = t;
                     tq[sl] = qq;
+#if SC_WIDECAP
+                    frame[sl] = t < n_tasks ? t / nN : (t - n_tasks) / nW;
+#else
                     frame[sl] = t / w.n_rows;
+#endif
                     level[sl] = rd.x;
                     ys[sl] = rd.y;
                     j0[sl] = min(nx, qq * nxs);
