@@ -208,6 +208,10 @@ int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, 
                                 /* chain launch (one-frame launches only)      */
 #define SC_INFO_CHAIN_SUBQ 10   /* dequeue sub-queues per XCD of the last chain  */
                                 /* launch (8 one-frame launches, 1 batches)    */
+#define SC_INFO_ITEM_FORM 11    /* integral cells and item form of the current */
+                                /* geometry: 1 channel-split cells, one lane   */
+                                /* per item; 2 interleaved 32-B cells, the     */
+                                /* lane-pair item form (sc_device.hpp)         */
 int sc_detector_info(sc_detector *d, int what, int64_t *value);
 
 /* ---- tuning and test options ---------------------------------------------

@@ -576,7 +576,8 @@ class Detector:
     # -- introspection ---------------------------------------------------------
     def info(self, key):
         keys = {"levels": 1, "grid_windows": 2, "rows": 3, "table_pitch": 4, "visited": 5, "fused_frames": 6,
-                "chain_waves": 7, "column_pass": 8, "spec_rounds": 9, "chain_subq": 10}
+                "chain_waves": 7, "column_pass": 8, "spec_rounds": 9, "chain_subq": 10,
+                "item_form": 11}
         v = ctypes.c_int64()
         _check(load_library().sc_detector_info(self._h, keys[key], ctypes.byref(v)))
         return v.value

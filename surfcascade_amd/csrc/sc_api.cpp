@@ -37,10 +37,12 @@ namespace {
 
 constexpr int kBandRows = 1;  // grid rows per cascade task (SC_BAND_ROWS overrides)
 constexpr bool kSplitLayout = true;  // table cell format (SC_OPT_TABLE_LAYOUT 1: interleaved)
-#if defined(SC_PAIR) && SC_PAIR
+#ifndef SC_PAIR
+#define SC_PAIR 1
+#endif
+#if SC_PAIR
 // the lane-pair item form (sc_device.hpp) runs on interleaved cells: chosen
-// for frame tables above 128 MiB (e.g. 4K), where sparse late-stage items
-// dominate the misses; SC_OPT_TABLE_LAYOUT 1 forces it for any frame
+// per frame size and model (build_geometry); SC_OPT_TABLE_LAYOUT 1 forces it
 constexpr bool kPairBigTables = true;
 #ifndef SC_PAIR_MIN_MIB  // (A/B: 0 puts every lazy-grid frame on the lane-pair form)
 #define SC_PAIR_MIN_MIB 128
@@ -303,9 +305,19 @@ void build_geometry(sc_detector *d, int W, int H) {
         t.Qp = (Q + 15) & ~15;
         t.rowp = 2 * t.ph * t.Qp;
         t.frame4 = (long long)(H + 1) * t.rowp;
-        const bool split = d->opt.table_layout ? false
-                                               : kSplitLayout && !(kPairBigTables && d->lazy &&
-                                                                   t.frame4 * 16 > ((long long)SC_PAIR_MIN_MIB << 20));
+        // the lane-pair item form (interleaved cells) wherever a batch's chain
+        // kernel is not the 16-wave one: tables beyond 128 MiB (C4: chain
+        // 23.02 vs 24.75 ms) and models whose LDS copy leaves 12 waves (C5:
+        // 21.41 vs 23.08 ms); the 16-wave kernel ties with it (C2 13.52 vs
+        // 13.48 ms), one-frame launches lose (0.588 vs 0.569 ms): split cells
+        // there (profiles/r6/e, f)
+        bool pair = kPairBigTables && d->lazy;
+        if (pair) {
+            const int l0 = (int)p.base_len, nx0 = l0 >= 1 && l0 <= W ? (W - l0) / ng.step + 1 : 1;
+            pair = t.frame4 * 16 > ((long long)SC_PAIR_MIN_MIB << 20) ||
+                   !sc::chain_batch_waves16(d->K, (nx0 + sc::kXcds - 1) / sc::kXcds, ng.n_levels, t.frame4);
+        }
+        const bool split = d->opt.table_layout ? false : kSplitLayout && !pair;
         t.cs = split ? 1 : 2;  // SC_OPT_TABLE_LAYOUT
         t.hs = split ? t.ph * t.Qp : 1;
         if ((long long)(H + 1) * t.rowp > (1ll << 28))  // byte offsets within a frame table: u32
@@ -1585,6 +1597,7 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value) {
         case SC_INFO_FUSED_FRAMES: *value = d->last_fused; break;
         case SC_INFO_CHAIN_WAVES: *value = d->last_waves; break;
         case SC_INFO_CHAIN_SUBQ: *value = d->last_subq; break;
+        case SC_INFO_ITEM_FORM: *value = d->geo.tg.cs; break;
         case SC_INFO_COLUMN_PASS: *value = d->last_colpass; break;
         case SC_INFO_SPEC_ROUNDS:  // the last chain launch's speculative rounds
             return guarded([&] {

@@ -314,8 +314,8 @@ __device__ __forceinline__ float lr_predict2(const f2 (&fp)[16], const float4 *w
     return (float)prob;
 }
 
-#ifndef SC_PAIR  // 1: lane-pair item form (interleaved 32-B cells); A/B variant, see pair_z32
-#define SC_PAIR 0
+#ifndef SC_PAIR  // 1: lane-pair item form on interleaved 32-B cells (pair_z32); 0: one-lane form only
+#define SC_PAIR 1
 #endif
 
 // ---- lane-pair item form (SC_PAIR) -------------------------------------------

@@ -294,6 +294,9 @@ constexpr double kRnSqrtLo = 0x1p-96, kRnSqrtHi = 0x1.fffffep127;  // sqrt_rn: [
 constexpr double kRnRcpLo = 0x1p-20, kRnRcpHi = 0x1p40;            // rcp_rn: [2^-20, 2^40]
 void launch_rn_check(int op, uint32_t lo, uint32_t hi, unsigned long long *out, int cus, hipStream_t s);
 size_t chain_lds_bytes(int K, int seg_max, int n_levels);
+// whether a multi-frame chain launch runs the 16-wave kernel (weights in LDS,
+// a table within 128 MiB); otherwise 10 (larger tables) or 12 waves
+bool chain_batch_waves16(int K, int row_max, int n_levels, long long frame4);
 size_t cascade_lds_bytes(int K, int strip_max, int band_rows);
 
 }  // namespace sc

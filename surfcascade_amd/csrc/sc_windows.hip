@@ -1516,6 +1516,12 @@ void launch_walk(const WalkArgs &a, int n_frames, hipStream_t s) {
     hipLaunchKernelGGL(walk_kernel, dim3(a.n_rows * n_frames), dim3(64), 0, s, a);
 }
 
+bool chain_batch_waves16(int K, int row_max, int n_levels, long long frame4) {
+    return frame4 * 16 <= (128ll << 20) &&
+           model_lds_bytes(K, true) + 16 * chain_wave_bytes(row_max) + n_levels * sizeof(LevelInfo) + 16 <=
+               160 * 1024;
+}
+
 int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hipStream_t s, int *waves_out) {
     auto scratch = [&](int nw) { return nw * chain_wave_bytes(w.row_max) + w.n_levels * sizeof(LevelInfo) + 16; };
     const size_t kLds = 160 * 1024;
@@ -1534,9 +1540,9 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hi
     // 24.92 at 8 and 25.22 at 12, profiles/r5/f; at 8 its widest levels 24-31
     // alone 7.58 vs 7.85 ms, levels 0-23 19.30 vs 18.45, profiles/r5/e).
     const bool fabric_bound = a.g.frame4 * 16 > (128ll << 20);
-    int nw = !fabric_bound && a.n_frames > 1 && model_lds_bytes(a.K, true) + scratch(16) <= kLds ? 16
-             : fabric_bound && a.n_frames > 1                                                  ? 10
-                                                                                               : 12;
+    int nw = a.n_frames > 1 && chain_batch_waves16(a.K, w.row_max, w.n_levels, a.g.frame4) ? 16
+             : fabric_bound && a.n_frames > 1                                                ? 10
+                                                                                             : 12;
     if (c.chain_waves == 8 || c.chain_waves == 10 || c.chain_waves == 12 ||
         ((c.chain_waves == 14 || c.chain_waves == 16) &&
          model_lds_bytes(a.K, false) + scratch(c.chain_waves) <= kLds))

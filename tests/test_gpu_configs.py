@@ -307,7 +307,7 @@ def test_c2_bench_form_exact(sc, oracle, face_cascade):
     ObjDetector.cpp:188-212)."""
     _bench_form_exact(sc, oracle, face_cascade, FACE_CFG, 1920, 1080, 32, sc.ScanParams(n_levels=24),
                       oracle.Params(n_levels=24),
-                      {"fused_frames": 30, "chain_waves": 16, "chain_subq": 1, "column_pass": 1}, (0, 2, 31))
+                      {"fused_frames": 30, "chain_waves": 16, "chain_subq": 1, "column_pass": 1, "item_form": 1}, (0, 2, 31))
 
 
 def test_c4_bench_form_exact(sc, oracle, face_cascade):
@@ -319,7 +319,7 @@ def test_c4_bench_form_exact(sc, oracle, face_cascade):
     detections of all 8."""
     _bench_form_exact(sc, oracle, face_cascade, FACE_CFG, 3840, 2160, 8, sc.ScanParams(n_levels=32),
                       oracle.Params(n_levels=32),
-                      {"fused_frames": 7, "chain_waves": 10, "chain_subq": 1}, (0, 1, 7))
+                      {"fused_frames": 7, "chain_waves": 10, "chain_subq": 1, "item_form": 2}, (0, 1, 7))
 
 
 def test_c5_bench_form_exact(sc, oracle, ped_cascade):
@@ -330,7 +330,7 @@ def test_c5_bench_form_exact(sc, oracle, ped_cascade):
     of frames 0, 2 and 31; visited sets and detections of all 32."""
     _bench_form_exact(sc, oracle, ped_cascade, PED_CFG, 1920, 1080, 32, sc.ScanParams.pedestrian(n_levels=23),
                       oracle.Params(base_len=64, aspect_h=2, n_levels=23),
-                      {"fused_frames": 30, "chain_waves": 12, "chain_subq": 1, "column_pass": 1}, (0, 2, 31))
+                      {"fused_frames": 30, "chain_waves": 12, "chain_subq": 1, "column_pass": 1, "item_form": 2}, (0, 2, 31))
 
 
 def test_one_frame_launch_uses_eight_subqueues(sc, oracle, face_cascade):
