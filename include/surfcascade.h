@@ -272,6 +272,10 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
                               /* done; tasks waiting for that frame's table    */
                               /* must time out and the next sync raise         */
                               /* SC_ERR_DEVICE (test-hook build only)          */
+#define SC_OPT_CHAIN_SPEC 23  /* one-frame chain launches: speculative rounds */
+                              /* (2 x 128 windows each) per waiting segment    */
+                              /* task: 0 auto (1 for a whole frame, the whole  */
+                              /* segment for a grid shard), or 1..64           */
 int sc_detector_set_option(sc_detector *d, int option, int64_t value);
 
 /* Enable per-window debug records (grid order) for the next detect calls. */

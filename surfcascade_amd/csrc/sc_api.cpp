@@ -152,6 +152,7 @@ struct sc_detector {
         int drop_handoff = -1;           // test only: task whose segment-0 hand-off is dropped (watchdog)
         int drop_walk = -1;              // test only: fused column walk whose completion count is dropped
         int chain_subq = 0;              // chain kernel dequeue sub-queues per XCD (0 auto: 8 one frame, else 1)
+        int chain_spec = 0;              // speculative rounds per waiting task of a one-frame launch (0 auto)
     } opt;
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
@@ -892,6 +893,11 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             // profiles/r5/l/split; 4 vs 1: 0.589 vs 0.606, profiles/r4/subq),
             // 1 for batches (C2 with 4: 17.0 vs 13.6 ms)
             wc.subq = d->opt.chain_subq ? d->opt.chain_subq : (nc == 1 ? 8 : 1);
+            // speculative rounds per waiting task (one-frame launches): 1 for
+            // a whole frame; a grid shard's launch has a fraction of the rows
+            // on the same waves, whose idle rounds then evaluate whole
+            // segments ahead of their entries (profiles/r6)
+            wc.spec_max = d->opt.chain_spec ? d->opt.chain_spec : (d->shard_world > 1 ? 64 : 1);
 #if defined(SC_WIDECAP) && SC_WIDECAP
             if (nc > 1 && wc.subq < sc::kMaxSubQ) {  // (the wide list's counter is sub-queue word kMaxSubQ - 1)
                 wc.n_wide = g.n_wide;
@@ -1683,6 +1689,7 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
                 regeo = false;
                 break;
             case SC_OPT_CHAIN_SUBQ: o.chain_subq = range(0, sc::kMaxSubQ); regeo = false; break;
+            case SC_OPT_CHAIN_SPEC: o.chain_spec = range(0, 64); regeo = false; break;
             case SC_OPT_CHAIN_WAVES:
                 o.chain_waves = range(0, 16);
                 if (o.chain_waves != 0 && o.chain_waves != 8 && o.chain_waves != 10 && o.chain_waves != 12 &&

@@ -204,6 +204,7 @@ struct WalkArgs {
     int n_wide;      // chain kernel, SC_WIDECAP builds: the last n_wide rows of `rows` are the wide levels',
                      // dealt from their own queue (sub-queue word kMaxSubQ - 1); 0: one list
     int wide_cap;    // ... at most wide_cap of a CU's task slots hold a wide row while narrow rows are left
+    int spec_max;    // chain kernel, one-frame launches: speculative rounds per waiting task (2*kBatch windows each)
     unsigned long long *prof;  // chain kernel, SC_PROF_CHAIN builds: phase cycle totals (or null)
     // Fused integral (chain kernel): colstrip's column walks of frames
     // [int_f0, n_frames) of this launch run inside the chain kernel as a

@@ -1045,7 +1045,11 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         return false;
     };
     int spec = -1;      // this round: speculative evaluation of waiting slot `spec` (both parities)
-    unsigned spd = 0;   // bit sl: slot sl's task was evaluated speculatively
+    // bit sl: slot sl's task was evaluated speculatively; bits 8 + 8 sl: its
+    // speculative rounds so far, each 2*kBatch windows (both parities) on
+    // from the segment start (at most w.spec_max rounds per task)
+    unsigned spd = 0;
+    auto spec_cur = [&](int sl) -> int { return (int)((spd >> (8 + 8 * sl)) & 0xFFu); };
     // the chain leaves slot sl's segment at absolute position pos: hand it on
 #if SC_PROF_CHAIN  // task trace (profiling builds): realtime stamps per task at dequeue / start / finish
     auto stamp = [&](int sl, int which) {
@@ -1118,7 +1122,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     j0[sl] = min(nx, qq * nxs);
                     nseg[sl] = min(nx, j0[sl] + nxs) - j0[sl];
                     st[sl] = 3;  // the poll below checks the frame, then starts segment 0
-                    spd &= ~(1u << sl);
+                    spd &= ~((1u << sl) | (0xFFu << (8 + 8 * sl)));
                     stamp(sl, 0);
                 }
                 SC_PROF(c_deq);
@@ -1151,18 +1155,23 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         }
         spec = -1;
         if (n_active == 0 && kSpec && a.n_frames == 1) {  // (one-frame launches: latency-bound)
-            // nothing to evaluate: the first waiting task not yet speculated
-            // gets both parities of its first 2*kBatch windows evaluated now,
-            // so its chain runs through them when its entry arrives (the
-            // hand-off chain's latency, not the work, sets a one-frame
-            // launch's tail)
+            // nothing to evaluate: the first waiting task with speculative
+            // rounds left gets both parities of its next 2*kBatch windows
+            // evaluated now, so its chain runs through them when its entry
+            // arrives (the hand-off chain's latency, not the work, sets a
+            // one-frame launch's tail).  w.spec_max rounds per task: 1 for a
+            // whole frame (more cost the windows the chain skips), all of the
+            // segment for a grid shard (few tasks per wave: the idle waves
+            // are free)
 #pragma unroll
             for (int sl = 0; sl < kSlots; sl++)
-                if (spec < 0 && st[sl] == 1 && !((spd >> sl) & 1u)) spec = sl;
+                if (spec < 0 && st[sl] == 1 && spec_cur(sl) < w.spec_max && spec_cur(sl) * 2 * kBatch < nseg[sl])
+                    spec = sl;
             if (spec >= 0) {
+                if (!((spd >> spec) & 1u))  // the task's first speculative round: its bits from zero
+                    for (int i = lane_id<RM>(); i < 3 * nwords; i += 64) bits0[spec * 3 * nwords + i] = 0ull;
                 spd |= 1u << spec;
                 nspec++;
-                for (int i = lane_id<RM>(); i < 3 * nwords; i += 64) bits0[spec * 3 * nwords + i] = 0ull;
             }
         }
         if (n_active == 0 && spec < 0) {
@@ -1225,7 +1234,8 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             if (lead_lane()) {
                 SlotDesc dd{};
                 if (SC_ACT(sl)) {
-                    const int lv = SC_OF(level, sl), rr = spec < 0 ? r[sl] : sl, ns_ = SC_OF(nseg, sl);
+                    const int lv = SC_OF(level, sl), ns_ = SC_OF(nseg, sl);
+                    const int rr = spec < 0 ? r[sl] : sl + 2 * kBatch * spec_cur(spec == 0 ? 0 : 1);
                     const LevelInfo &L = Lv[lv];
                     const int jb = SC_OF(j0, sl) + rr;  // the batch: jb, jb + 2, ...
                     dd.t_off = (unsigned)((long long)SC_OF(frame, sl) * g.frame4 + SC_OF(ys, sl) * g.rowp + g.win_cell(jb));
@@ -1307,6 +1317,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                                   (long long)(y / w.step) * L.nx + jj;
             unsigned long long *ev_ = evb(spec), *gd_ = gdb(spec), *dt_ = dtb(spec);
             float *sg = s_seg(spec);
+            const int k0 = 2 * kBatch * spec_cur(spec == 0 ? 0 : 1);  // the round's first window
 #pragma unroll
             for (int d = 0; d < 2; d++)
 #pragma unroll
@@ -1315,7 +1326,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     if (!mk) continue;
                     const bool in = (mk >> lane_id<RM>()) & 1ull;
                     const int u = c * 64 + lane_id<RM>();
-                    const int k = d + 2 * u;
+                    const int k = k0 + d + 2 * u;
                     bool good = false, det = false;
                     if (in) {
                         const int p = st_p[d * kBatch + u];
@@ -1333,13 +1344,14 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
                     }
                     const unsigned long long gm = __ballot(good), dm = __ballot(det);
                     if (lead_lane()) {
-                        const int base = d + 128 * c;
+                        const int base = k0 + d + 128 * c;
                         or_spread(ev_, base, mk);
                         if (gm) or_spread(gd_, base, gm);
                         if (dm) or_spread(dt_, base, dm);
                     }
                 }
             wave_sync();
+            spd += 1u << (8 + 8 * (spec == 0 ? 0 : 1));  // the task's next round starts 2*kBatch on
             SC_PROF(c_merge);
             continue;
         }

@@ -279,6 +279,51 @@ def test_speculative_rounds_run_and_match(sc, oracle, face_cascade, segs):
     assert dets[0].info("spec_rounds") > 0
 
 
+@pytest.mark.parametrize("spec", ["2", "64"])
+def test_speculation_depth(sc, oracle, face_cascade, spec):
+    """SC_OPT_CHAIN_SPEC: a waiting task gets up to `spec` speculative rounds,
+    each the next 2 x 128 windows of its segment (both parities), merged into
+    its bits at the round's offset; 64 evaluates whole segments ahead of their
+    entries.  More rounds run than with the default 1, and every evaluated
+    window, the visited set and the detections stay the oracle's."""
+    img = _frame(1920, 1080, 1000)
+    dets = []
+    _grid_parity(sc, oracle, face_cascade, FACE_CFG, img, sc.ScanParams(n_levels=24),
+                 oracle.Params(n_levels=24), det_out=dets, chain_spec=int(spec))
+    base = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=24))
+    base.detect(img)
+    assert dets[0].info("spec_rounds") > base.info("spec_rounds") > 0
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_one_frame_grid_shards_speculate(sc, oracle, face_cascade, world):
+    """The single-frame grid split as bench.py --shard grid runs it: rank r of
+    W scans rows i % W == r of ONE frame in a one-frame launch, whose idle
+    waves speculate whole segments (SC_OPT_CHAIN_SPEC auto for a shard).
+    Each rank's evaluated windows are the oracle's; the union of the ranks'
+    windows and their visited counts are the unsharded result, W = 2 / 4 / 8."""
+    img = _frame(1920, 1080, 1000)
+    params = oracle.Params(n_levels=24)
+    T = oracle.integral(img)
+    ref, nv = oracle.detect(T, face_cascade, params)
+    rp, rs = oracle.eval_grid(T, face_cascade, params)
+    det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=24))
+    det.set_debug(True)
+    got, vsum = [], 0
+    for rank in range(world):
+        det.set_shard(rank, world)
+        wins = det.detect(img)
+        assert det.info("spec_rounds") > 0
+        p, s, _v = det.dump_grid()
+        ev = p != -2
+        np.testing.assert_array_equal(p[ev], rp[ev])
+        assert s[ev].view(np.uint32).tobytes() == rs[ev].view(np.uint32).tobytes()
+        got += _det_set(wins)
+        vsum += det.info("visited")
+    assert sorted(got) == _det_set(ref)
+    assert vsum == nv
+
+
 @pytest.mark.parametrize("lds_weights", [None, "0"])
 def test_pedestrian_64x128(sc, oracle, ped_cascade, lds_weights):
     # lds_weights 0: the cache-read weights variant (models too big for the LDS)
