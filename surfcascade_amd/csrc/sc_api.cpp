@@ -881,7 +881,10 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
                 wc.stride = stride;
                 wc.carry = d->d_carry.p + f0 * carry_frame;
                 wc.int_f0 = pre;
-                wc.walks_per_frame = 2 * ((W + 2 * sc::kStrip - 1) / (2 * sc::kStrip));
+                // a wave per (64-column strip, channel half); interleaved cells:
+                // per 32-column strip, both halves (sc_windows.hip fused_walk)
+                wc.walks_per_frame = g.tg.cs == 2 ? (W + sc::kStrip - 1) / sc::kStrip
+                                                  : 2 * ((W + 2 * sc::kStrip - 1) / (2 * sc::kStrip));
                 wc.int_walks = (nc - pre) * wc.walks_per_frame;
                 d->last_fused += nc - pre;
             }

@@ -34,6 +34,22 @@ __device__ __forceinline__ Px4 load_px(const uint8_t *img, int stride, int W, in
     return v;
 }
 
+// load_px with h per lane (the interleaved-cell walk: both halves in one
+// wave): the same four bytes through selected addresses, no divergent branch
+__device__ __forceinline__ Px4 load_px_lanes(const uint8_t *img, int stride, int W, int H, int y, int x,
+                                             int h) {
+    const int xp = x > 0 ? x - 1 : 0, xn = x < W - 1 ? x + 1 : W - 1;
+    const uint8_t *rc = img + (long long)y * stride;
+    const uint8_t *ru = img + (long long)(y > 0 ? y - 1 : 0) * stride;
+    const uint8_t *rd = img + (long long)(y < H - 1 ? y + 1 : H - 1) * stride;
+    Px4 v;
+    v.a = (h ? ru : rc)[xp];
+    v.b = (h ? rd : rc)[xn];
+    v.c = (h ? rd : ru)[h ? xp : x];
+    v.d = (h ? ru : rd)[h ? xn : x];
+    return v;
+}
+
 // plane 2k = sat(Ip - In), plane 2k+1 = sat(In - Ip)  
 __device__ __forceinline__ uint2 grad_packed(const Px4 &v) {
     // half 0: (Ip, In) = (I[y][x-1], I[y][x+1]) and (I[y-1][x], I[y+1][x])

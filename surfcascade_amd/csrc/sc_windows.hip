@@ -713,14 +713,23 @@ static_assert((kWalkRows & (kWalkRows - 1)) == 0 && kWalkRows <= 64, "walk block
 #define SC_WALK_STORE 1
 #endif
 
+// INTER (interleaved 32-B cells, TableGeom cs 2): one wave per (frame,
+// 32-column strip), lanes 0-31 channel half 0 and lanes 32-63 half 1 of the
+// same columns, so each store instruction writes whole 32-B cells (with a
+// wave per half, two waves wrote the two halves of every cell: a C2 launch
+// with interleaved cells took 13.61 vs 12.84 ms unfused, profiles/r6/h);
+// two 32-lane scans, each half's carries read from its own lanes.
+template <bool INTER>
 __device__ __forceinline__ void fused_walk(const CascadeArgs &a, const WalkArgs &w, int t) {
     using namespace idev;
     const int fi = t / w.walks_per_frame, rem = t - fi * w.walks_per_frame;
-    const int f = w.int_f0 + fi, s = rem >> 1, h = rem & 1;
     const TableGeom g = a.g;
     const int W = g.W, H = g.H, ns = (W + kStrip - 1) / kStrip;
     const int lane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    const int x = s * 2 * kStrip + lane;
+    const int f = w.int_f0 + fi;
+    const int s = INTER ? rem : rem >> 1;              // 32-px strip (INTER) / 64-px strip
+    const int h = INTER ? lane >> 5 : rem & 1;         // channel half: per lane (INTER) / per wave
+    const int x = INTER ? s * kStrip + (lane & 31) : s * 2 * kStrip + lane;
     const bool live = x < W;
     const int xs = live ? x : W - 1;  // dead lanes still join the scan with zeros
     const uint8_t *img = w.frames + (long long)f * w.frame_bytes;
@@ -733,11 +742,13 @@ __device__ __forceinline__ void fused_walk(const CascadeArgs &a, const WalkArgs 
     unsigned off = (unsigned)g.at(x + 1, h) * 16u + rowb;  // table row 1 of the column
     // the exclusive carry at column 64*s is the 32-px strip 2*s's
     const uint4 *cin = reinterpret_cast<const uint4 *>(w.carry) + (long long)f * H * ns * 2 +
-                       (long long)(2 * s) * 2 + h;
+                       (long long)(INTER ? s : 2 * s) * 2 + h;
     auto load_block = [&](int y0, Px4 (&px)[kWalkRows], uint4 &cr) {
 #pragma unroll
-        for (int k = 0; k < kWalkRows; k++) px[k] = load_px(img, w.stride, W, H, min(y0 + k, H - 1), xs, h);
-        cr = cin[(long long)min(y0 + (lane & (kWalkRows - 1)), H - 1) * ns * 2];  // lane k: row y0 + k
+        for (int k = 0; k < kWalkRows; k++)
+            px[k] = INTER ? load_px_lanes(img, w.stride, W, H, min(y0 + k, H - 1), xs, h)
+                          : load_px(img, w.stride, W, H, min(y0 + k, H - 1), xs, h);
+        cr = cin[(long long)min(y0 + (lane & (kWalkRows - 1)), H - 1) * ns * 2];  // lane k (32 + k): row y0 + k
     };
     Px4 pa[kWalkRows];
     uint4 ca;
@@ -750,12 +761,24 @@ __device__ __forceinline__ void fused_walk(const CascadeArgs &a, const WalkArgs 
 #pragma unroll
         for (int k = 0; k < kWalkRows; k++) {
             uint2 p = live ? grad_packed(pa[k]) : make_uint2(0u, 0u);
-            p.x = wave_scan(p.x);  // 16-bit channel pairs: 64 px x 255 < 2^16
-            p.y = wave_scan(p.y);
-            S0 = S0 + (float)((uint32_t)__builtin_amdgcn_readlane((int)ca.x, k) + (p.x & 0xffffu));
-            S1 = S1 + (float)((uint32_t)__builtin_amdgcn_readlane((int)ca.y, k) + (p.x >> 16));
-            S2 = S2 + (float)((uint32_t)__builtin_amdgcn_readlane((int)ca.z, k) + (p.y & 0xffffu));
-            S3 = S3 + (float)((uint32_t)__builtin_amdgcn_readlane((int)ca.w, k) + (p.y >> 16));
+            if (INTER) {
+                p.x = half_scan(p.x);
+                p.y = half_scan(p.y);
+            } else {
+                p.x = wave_scan(p.x);  // 16-bit channel pairs: 64 px x 255 < 2^16
+                p.y = wave_scan(p.y);
+            }
+            // this row's strip carry: lane k's (half 0) or lane 32 + k's (half 1)
+            auto carry = [&](uint32_t c) -> uint32_t {
+                const uint32_t c0 = (uint32_t)__builtin_amdgcn_readlane((int)c, k);
+                if (!INTER) return c0;
+                const uint32_t c1 = (uint32_t)__builtin_amdgcn_readlane((int)c, 32 + k);
+                return h ? c1 : c0;
+            };
+            S0 = S0 + (float)(carry(ca.x) + (p.x & 0xffffu));
+            S1 = S1 + (float)(carry(ca.y) + (p.x >> 16));
+            S2 = S2 + (float)(carry(ca.z) + (p.y & 0xffffu));
+            S3 = S3 + (float)(carry(ca.w) + (p.y >> 16));
             if (live && y0 + k < H) {  // rows past H: harmless extra steps, not stored
                 typedef unsigned v4u __attribute__((ext_vector_type(4)));
                 const v4u v = {__float_as_uint(S0), __float_as_uint(S1), __float_as_uint(S2), __float_as_uint(S3)};
@@ -902,7 +925,8 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
             t = __builtin_amdgcn_readfirstlane(t);
             if (t >= w.int_walks) break;
 #ifndef SC_NO_WALK
-            fused_walk(a, w, t);
+            if (a.g.cs == 2) fused_walk<true>(a, w, t);
+            else fused_walk<false>(a, w, t);
 #endif
         }
         __builtin_amdgcn_s_setprio(0);

@@ -12,6 +12,8 @@ Bit-exact: integral tables, per-window stage reached and last-stage score
 bits of every evaluated window, the visited set, detections with their f64
 scores (ObjDetector.cpp:174-220).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -266,6 +268,8 @@ def _bench_form_exact(sc, oracle, cascade, model, W, H, n, params_sc, params_or,
     counts = torch.zeros(n + 1, dtype=torch.int32, device="cuda:0")
     det.enqueue_device(frames, recs, counts)
     det.synchronize()
+    if os.environ.get("SC_TEST_ANY_ITEM_FORM"):  # A/B variant runs (profiles/r6): the form is the variant's
+        expect = {k: v for k, v in expect.items() if k != "item_form"}
     for k, v in expect.items():
         assert det.info(k) == v, (k, det.info(k))
     got = merge_records([counts.cpu().numpy()], [recs.cpu().numpy()], [0])
