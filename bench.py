@@ -434,6 +434,9 @@ def main():
     kt = det.get_timing()
     visited = det.info("visited")
     fused_frames = det.info("fused_frames")  # (before the latency / host legs replace the last call)
+    # the launch shape of the timed step: chain-kernel waves per CU, and the
+    # item form (1 split cells, one lane per item; 2 interleaved cells, lane pairs)
+    shape = {"chain_waves": det.info("chain_waves"), "item_form": det.info("item_form")}
     if dist is None:
         check_capacity()
     else:  # the last timed step's gather (raises if any rank's buffer overflowed)
@@ -518,7 +521,7 @@ def main():
                        "frames_per_gpu_per_step": B, "grid_windows_per_frame": grid,
                        "levels": args.levels,
                        "parallelism": ("grid-row-sharded x%d" if grid_shard else "frame-sharded dp%d")
-                       % world},
+                       % world, **shape},
             "roofline": roofline(achieved, traffic, valu_insts, avg_win_s, win_bytes, pipe_bytes * B,
                                  pipe_s, pmc, opts, fused),
             "kernel_ms_per_launch": {k: v[0] / max(v[1], 1) for k, v in kt.items()},
