@@ -1575,9 +1575,12 @@ int launch_chain(const CascadeArgs &a, const WalkArgs &w, const LaunchCfg &c, hi
     // per launch: 10 (fewer rows in flight per XCD: C4 24.70 ms per launch vs
     // 24.92 at 8 and 25.22 at 12, profiles/r5/f; at 8 its widest levels 24-31
     // alone 7.58 vs 7.85 ms, levels 0-23 19.30 vs 18.45, profiles/r5/e).
+    // With the lane-pair item form (interleaved cells, cs 2: §3 of DESIGN.md)
+    // such tables run 12 waves again: C4 21.80 vs 22.52 ms at 10, 22.10 at
+    // 14, 24.39 at 8 (profiles/r6/n); 10 stays for the one-lane form.
     const bool fabric_bound = a.g.frame4 * 16 > (128ll << 20);
     int nw = a.n_frames > 1 && chain_batch_waves16(a.K, w.row_max, w.n_levels, a.g.frame4) ? 16
-             : fabric_bound && a.n_frames > 1                                                ? 10
+             : fabric_bound && a.n_frames > 1 && a.g.cs == 1                                 ? 10
                                                                                              : 12;
     if (c.chain_waves == 8 || c.chain_waves == 10 || c.chain_waves == 12 ||
         ((c.chain_waves == 14 || c.chain_waves == 16) &&

@@ -114,8 +114,9 @@ def test_c5_bench_form_fused_12_waves(sc, oracle, ped_cascade):
 
 def test_c4_bench_form_colstrip_one_launch(sc, oracle, face_cascade):
     """C4's form below 4 frames per call: several 4K frames x 32 levels in
-    ONE chain launch (10 waves, tables beyond the Infinity Cache, no fusion)
-    whose tables colstrip built.  Lowered thetas so every
+    ONE chain launch (tables beyond the Infinity Cache: interleaved cells, the
+    lane-pair item form at 12 waves; no fusion) whose tables colstrip built
+    (VERDICT r3 weak #1).  Lowered thetas so every
     level reaches detections."""
     from surfcascade_amd import synth
     c = face_cascade
@@ -126,13 +127,13 @@ def test_c4_bench_form_colstrip_one_launch(sc, oracle, face_cascade):
                                sc.ScanParams(n_levels=32), oracle.Params(n_levels=32), integral_passes=1)
     assert det.info("column_pass") == 2  # colstrip
     assert det.info("fused_frames") == 0
-    assert det.info("chain_waves") == 10  # tables beyond the Infinity Cache, 2+ frames
+    assert det.info("chain_waves") == 12 and det.info("item_form") == 2  # tables beyond the Infinity Cache
     assert all(len(b) > 100 for b in batch)
 
 
 def test_c4_bench_form_fused_one_prebuilt(sc, oracle, face_cascade):
     """C4 exactly as bench.py runs it, in small: 4K frames x 32 levels in one
-    10-wave chain launch whose first frame is integrated before it (two-pass;
+    12-wave lane-pair chain launch whose first frame is integrated before it (two-pass;
     one prebuilt frame since a 4K table is larger than 128 MiB) and whose
     other frames' column walks run inside the chain kernel.  Lowered thetas
     so every level reaches detections."""
@@ -145,7 +146,7 @@ def test_c4_bench_form_fused_one_prebuilt(sc, oracle, face_cascade):
                                sc.ScanParams(n_levels=32), oracle.Params(n_levels=32))
     assert det.info("fused_frames") == 3
     assert det.info("column_pass") == 1  # the prebuilt frame: rowcarry R rows + colsum
-    assert det.info("chain_waves") == 10
+    assert det.info("chain_waves") == 12 and det.info("item_form") == 2
     assert all(len(b) > 100 for b in batch)
 
 
@@ -318,12 +319,12 @@ def test_c4_bench_form_exact(sc, oracle, face_cascade):
     """C4 exactly as bench.py measures it: 8 device-resident 4K frames x 32
     levels (l up to 1343, sums past 2^24) in ONE call with the calibrated
     model: one frame integrated before the chain kernel (a 4K table is larger
-    than 128 MiB), the column walks of the other 7 inside it, 10 waves.
+    than 128 MiB), the column walks of the other 7 inside it, 12 waves, lane pairs.
     Tables and per-window bits of frames 0, 1 and 7; visited sets and
     detections of all 8."""
     _bench_form_exact(sc, oracle, face_cascade, FACE_CFG, 3840, 2160, 8, sc.ScanParams(n_levels=32),
                       oracle.Params(n_levels=32),
-                      {"fused_frames": 7, "chain_waves": 10, "chain_subq": 1, "item_form": 2}, (0, 1, 7))
+                      {"fused_frames": 7, "chain_waves": 12, "chain_subq": 1, "item_form": 2}, (0, 1, 7))
 
 
 def test_c5_bench_form_exact(sc, oracle, ped_cascade):
