@@ -265,7 +265,7 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
                               /* the test-hook build (lib/testhooks) accepts */
                               /* a value other than -1                       */
 #define SC_OPT_CHAIN_SUBQ 21  /* chain kernel dequeue counters per XCD queue: */
-                              /* 0 auto (8 for a one-frame launch, else 1),    */
+                              /* 0 auto (4 for a one-frame launch, else 1),    */
                               /* or 1..8                                       */
 #define SC_OPT_TEST_DROP_WALK 22 /* test only (-1 off): the fused column walk  */
                               /* `value` of every launch does not count itself */
@@ -276,6 +276,8 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
                               /* (2 x 128 windows each) per waiting segment    */
                               /* task: 0 auto (1 for a whole frame, the whole  */
                               /* segment for a grid shard), or 1..64           */
+#define SC_OPT_CHAIN_SLOTS 24 /* chain kernel task slots per wave: 0 auto (1   */
+                              /* for a one-frame launch, 2 for batches), 1, 2  */
 int sc_detector_set_option(sc_detector *d, int option, int64_t value);
 
 /* Enable per-window debug records (grid order) for the next detect calls. */

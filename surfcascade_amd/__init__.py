@@ -51,7 +51,7 @@ OPTIONS = {"full_grid": 1, "chunk_min": 2, "table_layout": 3, "phases": 4, "subs
            "level_lo": 15, "level_hi": 16, "chain_waves": 17,
            "integral_fuse": 18, "integral_pre": 19,
            "test_drop_handoff": 20, "chain_subq": 21, "test_drop_walk": 22,
-           "chain_spec": 23}
+           "chain_spec": 23, "chain_slots": 24}
 
 # every symbol include/surfcascade.h declares
 EXPORTS = ("sc_scan_params_default", "sc_model_load", "sc_model_parse", "sc_model_save",

@@ -151,8 +151,9 @@ struct sc_detector {
         int integral_pre = 0;            // fused: frames integrated before the chain kernel (0: 2)
         int drop_handoff = -1;           // test only: task whose segment-0 hand-off is dropped (watchdog)
         int drop_walk = -1;              // test only: fused column walk whose completion count is dropped
-        int chain_subq = 0;              // chain kernel dequeue sub-queues per XCD (0 auto: 8 one frame, else 1)
+        int chain_subq = 0;              // chain kernel dequeue sub-queues per XCD (0 auto: 4 one frame, else 1)
         int chain_spec = 0;              // speculative rounds per waiting task of a one-frame launch (0 auto)
+        int chain_slots = 0;             // task slots per wave of the chain kernel (0 auto: 1 one frame, 2 batches)
     } opt;
     int shard_rank = 0, shard_world = 1;  // grid sharding: rows i with i % world == rank
     // geometry on device
@@ -891,11 +892,17 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
             wc.frame0 = f0;
             wc.drop_task1 = d->opt.drop_handoff + 1;  // SC_OPT_TEST_DROP_HANDOFF (0: none)
             wc.drop_walk1 = d->opt.drop_walk + 1;     // SC_OPT_TEST_DROP_WALK (0: none)
-            // dequeue sub-queues (SC_OPT_CHAIN_SUBQ): 8 for a one-frame launch
-            // (chain kernel 0.573 vs 0.582 ms with 4 per 1080p frame,
-            // profiles/r5/l/split; 4 vs 1: 0.589 vs 0.606, profiles/r4/subq),
-            // 1 for batches (C2 with 4: 17.0 vs 13.6 ms)
-            wc.subq = d->opt.chain_subq ? d->opt.chain_subq : (nc == 1 ? 8 : 1);
+            // task slots per wave (SC_OPT_CHAIN_SLOTS): a one-frame launch is
+            // latency-bound by its rows' hand-off chains, and one task per wave
+            // runs each task at the wave's full speed (one frame: chain 0.532
+            // vs 0.574 ms with 2); a batch wants two tasks sharing each round
+            // (C2 14.12 vs 13.53 ms with 1) (profiles/r6/p)
+            wc.slots = d->opt.chain_slots ? d->opt.chain_slots : (nc == 1 ? 1 : 2);
+            // dequeue sub-queues (SC_OPT_CHAIN_SUBQ): for a one-frame launch 4
+            // with one task per wave (chain 0.5249 vs 0.5324 ms with 8, 0.5310
+            // with 1, profiles/r6/r), 8 with two (0.573 vs 0.582 ms with 4,
+            // profiles/r5/l/split); 1 for batches (C2 with 4: 17.0 vs 13.6 ms)
+            wc.subq = d->opt.chain_subq ? d->opt.chain_subq : (nc == 1 ? (wc.slots == 1 ? 4 : 8) : 1);
             // speculative rounds per waiting task (one-frame launches): 1 for
             // a whole frame; a grid shard's launch has a fraction of the rows
             // on the same waves, whose idle rounds then evaluate whole
@@ -1693,6 +1700,7 @@ int sc_detector_set_option(sc_detector *d, int option, int64_t value) {
                 break;
             case SC_OPT_CHAIN_SUBQ: o.chain_subq = range(0, sc::kMaxSubQ); regeo = false; break;
             case SC_OPT_CHAIN_SPEC: o.chain_spec = range(0, 64); regeo = false; break;
+            case SC_OPT_CHAIN_SLOTS: o.chain_slots = range(0, 2); regeo = false; break;
             case SC_OPT_CHAIN_WAVES:
                 o.chain_waves = range(0, 16);
                 if (o.chain_waves != 0 && o.chain_waves != 8 && o.chain_waves != 10 && o.chain_waves != 12 &&

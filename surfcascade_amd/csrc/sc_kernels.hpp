@@ -200,11 +200,12 @@ struct WalkArgs {
     int frame0;      // chain kernel: first frame of this launch (record frame index)
     int nseg;        // chain kernel: segments per row (8; 4 for one-frame launches)
     int seg_shift;   // chain kernel: log2(kXcds / nseg)
-    int subq;        // chain kernel: dequeue counters per XCD queue (1..kMaxSubQ; 8 for one-frame launches)
+    int subq;        // chain kernel: dequeue counters per XCD queue (1..kMaxSubQ; 4 for one-frame launches)
     int n_wide;      // chain kernel, SC_WIDECAP builds: the last n_wide rows of `rows` are the wide levels',
                      // dealt from their own queue (sub-queue word kMaxSubQ - 1); 0: one list
     int wide_cap;    // ... at most wide_cap of a CU's task slots hold a wide row while narrow rows are left
     int spec_max;    // chain kernel, one-frame launches: speculative rounds per waiting task (2*kBatch windows each)
+    int slots;       // chain kernel: task slots a wave fills (1 or kSlots = 2)
     unsigned long long *prof;  // chain kernel, SC_PROF_CHAIN builds: phase cycle totals (or null)
     // Fused integral (chain kernel): colstrip's column walks of frames
     // [int_f0, n_frames) of this launch run inside the chain kernel as a

@@ -1129,7 +1129,7 @@ __global__ __launch_bounds__(64 * NW, 1) void chain_kernel(CascadeArgs a, WalkAr
         int n_active = 0, n_wait = 0;
 #pragma unroll
         for (int sl = 0; sl < kSlots; sl++) {
-            if (st[sl] == 0) {
+            if (st[sl] == 0 && sl < w.slots) {  // (w.slots 1: the second slot stays empty)
                 int t, qq;
                 int2 rd;
                 if (dequeue(t, qq, rd)) {

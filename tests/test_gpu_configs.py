@@ -338,21 +338,22 @@ def test_c5_bench_form_exact(sc, oracle, ped_cascade):
                       {"fused_frames": 30, "chain_waves": 12, "chain_subq": 1, "column_pass": 1, "item_form": 2}, (0, 2, 31))
 
 
-def test_one_frame_launch_uses_eight_subqueues(sc, oracle, face_cascade):
-    """One-frame launches deal their tasks through 8 dequeue sub-queues per
-    XCD (SC_INFO_CHAIN_SUBQ), each of the two XCDs of a segment over its own
-    contiguous part of the row list; batches through one; results are the
-    oracle's at every sub-queue count (SC_OPT_CHAIN_SUBQ)."""
+def test_one_frame_launch_subqueues(sc, oracle, face_cascade):
+    """One-frame launches deal their tasks through 4 dequeue sub-queues per
+    XCD (SC_INFO_CHAIN_SUBQ; one task per wave, SC_OPT_CHAIN_SLOTS), each of
+    the two XCDs of a segment over its own contiguous part of the row list;
+    batches through one; results are the oracle's at every sub-queue count
+    (SC_OPT_CHAIN_SUBQ) and with two task slots per wave."""
     img = _frame(1920, 1080, 1234)
     params = oracle.Params(n_levels=24)
     T = oracle.integral(img)
     ref, nv = oracle.detect(T, face_cascade, params)
     rp, rs = oracle.eval_grid(T, face_cascade, params)
-    for q in (0, 1, 2, 3, 8):
-        det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=24)).set_options(chain_subq=q)
+    for q, slots in ((0, 0), (1, 0), (2, 0), (3, 0), (8, 0), (0, 2), (8, 2)):
+        det = sc.Detector(FACE_CFG, sc.ScanParams(n_levels=24)).set_options(chain_subq=q, chain_slots=slots)
         det.set_debug(True)
         wins = det.detect(img)
-        assert det.info("chain_subq") == (8 if q == 0 else q)
+        assert det.info("chain_subq") == (q if q else (8 if slots == 2 else 4))
         p, s, _v = det.dump_grid()
         ev = p != -2
         np.testing.assert_array_equal(p[ev], rp[ev])
