@@ -207,7 +207,7 @@ int sc_mine_batch_device(sc_detector *d, const uint8_t *d_frames, int n, int w, 
 #define SC_INFO_SPEC_ROUNDS 9   /* speculative evaluation rounds of the last    */
                                 /* chain launch (one-frame launches only)      */
 #define SC_INFO_CHAIN_SUBQ 10   /* dequeue sub-queues per XCD of the last chain  */
-                                /* launch (8 one-frame launches, 1 batches)    */
+                                /* launch (4 one-frame launches, 1 batches)    */
 #define SC_INFO_ITEM_FORM 11    /* integral cells and item form of the current */
                                 /* geometry: 1 channel-split cells, one lane   */
                                 /* per item; 2 interleaved 32-B cells, the     */
@@ -242,7 +242,8 @@ int sc_detector_info(sc_detector *d, int what, int64_t *value);
 #define SC_OPT_WGS_PER_CU 11  /* workgroups per CU, 0 = occupancy limit        */
 #define SC_OPT_PROFILE 12     /* chain-kernel phase counters (profiling builds) */
 #define SC_OPT_CHAIN_SEGS 13  /* chain kernel: segments per row (0 auto: 4 for a */
-                              /* one-frame launch, else 8; or 1, 2, 4, 8)      */
+                              /* one-frame launch of fewer than 8 grid shards, */
+                              /* else 8; or 1, 2, 4, 8)                        */
 #define SC_OPT_INTEGRAL_PASSES 14 /* integral: 0 auto (two passes up to 3     */
                               /* frames), 1 colstrip, 2 rowfull + colsum       */
 #define SC_OPT_LEVEL_LO 15    /* scan only levels >= LEVEL_LO (default 0)      */

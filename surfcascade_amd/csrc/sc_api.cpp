@@ -694,11 +694,13 @@ void enqueue(sc_detector *d, const uint8_t *d_frames, int n, int W, int H, int s
     // byte offsets); rows cut into 8 segments (one per XCD), or 4 for a
     // one-frame launch, whose time the segment hand-off chain's fill and
     // drain dominate (0.73 vs 0.83 ms per 1080p frame; 8 win from 2 frames
-    // on)
+    // on) and for a one-frame grid shard of 8 or more
+    // ranks, whose few rows make the segment-0 evaluation the serial floor
+    // (C2 W = 8 chain 0.239 vs 0.253 ms, profiles/r6/o)
     int chunk = (int)std::max<long long>(1, (1ll << 28) / g.tg.frame4);
     if (d->opt.chain_chunk > 0) chunk = std::min(chunk, d->opt.chain_chunk);  // SC_OPT_CHAIN_CHUNK
     auto segs_for = [&](int frames) {  // SC_OPT_CHAIN_SEGS overrides
-        return d->opt.chain_segs ? d->opt.chain_segs : (frames == 1 ? sc::kXcds / 2 : sc::kXcds);
+        return d->opt.chain_segs ? d->opt.chain_segs : (frames == 1 && d->shard_world < 8 ? sc::kXcds / 2 : sc::kXcds);
     };
     auto seg_max_for = [&](int s) { return (g.nx_max + s - 1) / s; };
     const int last = n % chunk ? n % chunk : std::min(chunk, n);

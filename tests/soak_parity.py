@@ -59,7 +59,9 @@ def run_case(sc, O, synth, models, case, seed, stats):
             "chain_subq": int(rng.choice([0, 1, 2, 3, 4, 8])),
             "integral_fuse": int(rng.choice([0, 1, 2])),
             "integral_pre": int(rng.choice([0, 1, 2, 3])),
-            "table_layout": int(rng.choice([0, 1]))}  # 1: interleaved cells, the lane-pair item form
+            "table_layout": int(rng.choice([0, 1])),  # 1: interleaved cells, the lane-pair item form
+            "chain_slots": int(rng.choice([0, 1, 2])),
+            "chain_spec": int(rng.choice([0, 1, 2, 64]))}
     frames = np.stack([synth.make_frame(W, H, 20000 + 17 * case + k) for k in range(n)])
     desc = dict(case=case, W=W, H=H, n=n, ped=ped, base=base, step=step, pk=pk, ss=ss, levels=levels,
                 permissive=bool(theta is not c.theta), **opts)
