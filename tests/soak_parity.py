@@ -3,7 +3,8 @@ through the C ABI against the oracle -- frame size, frames per call, levels,
 base window, step, prefilter factor, stride threshold, permissive or model
 thetas, face or pedestrian model, and the schedule options that must never
 change a bit (chain waves, dequeue sub-queues, integral fusion and prebuilt
-frames).  Every frame: visited count, visited set and detections (f64 scores);
+frames, the cell layout, task slots per wave, speculation depth); about one
+case in ten is a single large frame (2048-4200 px wide).  Every frame: visited count, visited set and detections (f64 scores);
 every 4th case also the integral table and per-window stage / score bits.
 
     python tests/soak_parity.py [--cases 300] [--seed 9000] [--out F]
@@ -35,8 +36,9 @@ def load_models(O):
     return models
 
 
-def run_case(sc, O, synth, models, case, seed, stats):
-    """One random case; returns None, or the case's description with the error."""
+def run_case(sc, O, synth, models, case, seed, stats, big_frames=True):
+    """One random case; returns None, or the case's description with the error.
+    big_frames: about 1 case in 10 is one frame of 2048-4200 x 700-2200 px."""
     rng = np.random.default_rng(seed + case)
     ped = rng.random() < 0.25
     c = models["ped64x128_synth.cfg" if ped else "face40_synth.cfg"]
@@ -62,6 +64,8 @@ def run_case(sc, O, synth, models, case, seed, stats):
             "table_layout": int(rng.choice([0, 1])),  # 1: interleaved cells, the lane-pair item form
             "chain_slots": int(rng.choice([0, 1, 2])),
             "chain_spec": int(rng.choice([0, 1, 2, 64]))}
+    if rng.random() < 0.1 and big_frames:  # one large frame: multi-chunk one-frame block sums, odd widths, tables > 128 MiB
+        W, H, n = int(rng.integers(2048, 4200)), int(rng.integers(700, 2200)), 1
     frames = np.stack([synth.make_frame(W, H, 20000 + 17 * case + k) for k in range(n)])
     desc = dict(case=case, W=W, H=H, n=n, ped=ped, base=base, step=step, pk=pk, ss=ss, levels=levels,
                 permissive=bool(theta is not c.theta), **opts)

@@ -23,6 +23,6 @@ def env(oracle):
 def test_random_schedule_sweep(env, case):
     sc, O, synth, models = env
     stats = {"frames": 0, "visited": 0, "detections": 0, "bits_checked": 0}
-    fail = soak_parity.run_case(sc, O, synth, models, case, 31000, stats)
+    fail = soak_parity.run_case(sc, O, synth, models, case, 31000, stats, big_frames=False)
     assert fail is None, fail
     assert stats["frames"] > 0
